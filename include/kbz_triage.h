@@ -1,0 +1,168 @@
+/*
+ * include/kbz_triage.h -- C ABI of libkbz_hip.so, the MI355X (gfx950) coverage-triage backend.
+ *
+ * Plain C types only (no torch, no HIP types): device pointers are `void *`/typed pointers to
+ * device memory, streams are `void *` holding a hipStream_t (NULL = the null stream).
+ *
+ * What each entry point replaces in the reference (paths relative to ThePatrickStar/killerbeez):
+ *
+ *   kbz_triage_batch_device / kbz_triage_batch_host
+ *       the per-exec novelty step, done for a whole ordered batch of traces:
+ *         instrumentation/afl_instrumentation.c:231-274   finish_fuzz_round (raw/simplify +
+ *                                                          has_new_bits vs 3 virgin maps)
+ *         instrumentation/afl_instrumentation.c:189-198   afl_is_new_path   (hnb != 0)
+ *         instrumentation/dynamorio_instrumentation.c:1428-1468 has_new_coverage (classify,
+ *                                                          hash32[_with_ignore], last-hash skip,
+ *                                                          has_new_bits[_with_ignore])
+ *       Results are bit-exact with running those functions once per trace, in batch order.
+ *   kbz_get_virgin / kbz_set_virgin
+ *       the virgin-map part of afl_get_state / afl_set_state (afl_instrumentation.c:62-109)
+ *   kbz_merge_and_device / kbz_merge_and_host
+ *       the merger fold merger/merger.c:79-99 -> afl_merge afl_instrumentation.c:123-140
+ *       (merge_bitmaps :116-121 == dynamorio_instrumentation.c:334-339)
+ *   kbz_hash32_device / kbz_xxh64_device
+ *       afl_progs/hash.h:36-65 (hash32) and instrumentation/xxhash.c:855 (XXH64, v0.6.5)
+ *       over every trace of a batch (crash/hang dedup keys).
+ *
+ * Conventions: every function returns 0 on success and -1 on failure (device errors are
+ * mapped to -1; kbz_last_error() gives a message).  Buffers are caller-owned.  One context
+ * per host thread; a context is bound to the device that was current at kbz_ctx_create.
+ * Nothing here blocks the host unless its name ends in _host or it copies to host memory.
+ */
+#ifndef KBZ_TRIAGE_H
+#define KBZ_TRIAGE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KBZ_ABI_VERSION 1
+
+/* Triage semantics (which reference code path a batch reproduces). */
+enum kbz_mode {
+  KBZ_MODE_AFL = 0,          /* afl_instrumentation.c finish_fuzz_round: EXIT raw -> virgin_bits,
+                                HANG simplify -> virgin_tmout, CRASH simplify -> virgin_crash,
+                                result 0/1/2 (last_is_new_path) */
+  KBZ_MODE_DYNAMORIO = 1,    /* dynamorio has_new_coverage: classify_counts, hash32 (or
+                                hash32_with_ignore), skip if hash == last hash, has_new_bits
+                                (or _with_ignore) vs virgin_bits; result 0/1/2, 0 when skipped */
+  KBZ_MODE_AFL_CLASSIFY = 2  /* afl-fuzz flavour (north_star): EXIT classify_counts -> virgin_bits,
+                                HANG/CRASH simplify -> virgin_tmout/virgin_crash */
+};
+
+/* Per-trace outcome, the FUZZ_* results of get_fuzz_result.  The numeric FUZZ_* values live
+ * in the external killerbeez-utils (not in the reference tree); these are ours. */
+enum kbz_outcome { KBZ_FUZZ_NONE = 0, KBZ_FUZZ_HANG = 1, KBZ_FUZZ_CRASH = 2 };
+
+/* Which per-trace outputs to produce (hnb is always produced). */
+enum kbz_want { KBZ_WANT_H32 = 1, KBZ_WANT_X64 = 2 };
+
+typedef struct kbz_ctx kbz_ctx_t;
+
+/* ---- context ------------------------------------------------------------------------------ */
+/* map_size: bytes per trace map, a multiple of 256 (64 KiB = AFL MAP_SIZE, config.h:314-315;
+ * 1 MiB = DynamoRIO/winafl-scale).  max_batch: largest n passed to a triage call.
+ * Virgin maps start all-0xff (setup_shm, afl_instrumentation.c:555-559), last hash 0. */
+kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch);
+void kbz_ctx_destroy(kbz_ctx_t *ctx);
+const char *kbz_last_error(void);
+int kbz_abi_version(void);
+
+/* ignore_bytes for KBZ_MODE_DYNAMORIO (dynamorio_instrumentation.c:788-814): map_size bytes of
+ * host memory, or NULL to clear.  Same conventions as the reference: hash32_with_ignore ANDs
+ * each trace word with the ignore word, has_new_bits_with_ignore only looks at bytes whose
+ * ignore byte is 0. */
+int kbz_set_ignore(kbz_ctx_t *ctx, const uint8_t *host_ignore);
+
+/* The three virgin maps, host memory, 3*map_size bytes: virgin_bits | virgin_tmout |
+ * virgin_crash.  DYNAMORIO mode uses only virgin_bits.  Synchronous. */
+int kbz_get_virgin(kbz_ctx_t *ctx, uint8_t *host_out);
+int kbz_set_virgin(kbz_ctx_t *ctx, const uint8_t *host_in);
+/* DynamoRIO last_shm_hash (dynamorio_instrumentation.c:1450-1461).  Synchronous. */
+int kbz_get_last_hash(kbz_ctx_t *ctx, uint32_t *out);
+int kbz_set_last_hash(kbz_ctx_t *ctx, uint32_t value);
+/* Device pointer to the current virgin maps (3*map_size bytes); valid until the next triage
+ * call (the context double-buffers them). */
+uint8_t *kbz_virgin_device(kbz_ctx_t *ctx);
+
+/* ---- batched triage ------------------------------------------------------------------------ */
+/* traces:   device, n rows of map_size raw 8-bit hit counters, row j at traces + j*stride
+ *           (stride a multiple of 16, base 16-byte aligned).  Not modified.
+ * outcome:  device int8[n] of kbz_outcome, or NULL (= all KBZ_FUZZ_NONE).
+ * hnb_out:  device uint8[n]: has_new_bits result of trace j given traces 0..j-1 (0/1/2).
+ * h32_out:  device uint32[n] or NULL: hash32 (HASH_CONST seed) of the transformed trace
+ *           (the value DynamoRIO compares with last_shm_hash).
+ * x64_out:  device uint64[n] or NULL (needs KBZ_WANT_X64): XXH64(seed 0) of the transformed
+ *           trace -- the crash/hang dedup key.
+ * Stream-ordered; the virgin maps and last hash advance as if the n execs ran in order. */
+int kbz_triage_batch_device(kbz_ctx_t *ctx, const uint8_t *traces, size_t n, size_t stride,
+                            const int8_t *outcome, uint8_t *hnb_out, uint32_t *h32_out,
+                            uint64_t *x64_out, int want, void *stream);
+
+/* Host-memory variant: streams the batch through pinned staging slots with double-buffered
+ * hipMemcpyAsync and overlaps copy-in with triage.  Blocks until results are in host memory. */
+int kbz_triage_batch_host(kbz_ctx_t *ctx, const uint8_t *traces, size_t n, size_t stride,
+                          const int8_t *outcome, uint8_t *hnb_out, uint32_t *h32_out,
+                          uint64_t *x64_out, int want);
+
+/* ---- sharded (multi-GPU) triage ------------------------------------------------------------ */
+/* A batch split into contiguous shards, one per GPU (rank g holds traces [lo_g, hi_g)), gives
+ * the same results as one kbz_triage_batch over the whole batch when each rank runs:
+ *   1. kbz_shard_begin(ctx, shard, ...)                 -- local streaming pass
+ *   2. all-gather of kbz_shard_last_hash (DYNAMORIO only), then kbz_shard_link(ctx, prev_last,
+ *      is_first_shard, global_last) with prev_last = pair of the nearest non-empty earlier
+ *      rank and global_last = pair of the last non-empty rank
+ *   3. kbz_shard_reduce(ctx)                            -- local OR aggregates
+ *   4. all-gather of kbz_shard_aggregate (nclass*map_size bytes per rank, device memory),
+ *      OR of the ranks before this one -> prefix, OR of all ranks -> total
+ *   5. kbz_shard_finish(ctx, prefix, total, hnb_out)    -- resolve + virgin update
+ * RCCL has no bitwise reductions, so step 4 is an all-gather plus a local OR (kbz_or_reduce).
+ * All pointers device memory, all calls stream-ordered on `stream`. */
+int kbz_shard_begin(kbz_ctx_t *ctx, const uint8_t *traces, size_t n, size_t stride,
+                    const int8_t *outcome, uint32_t *h32_out, uint64_t *x64_out, int want,
+                    void *stream);
+/* Copies {h32 of this shard's last trace, n != 0} into device uint32 d_out[2]. */
+int kbz_shard_last_hash(kbz_ctx_t *ctx, uint32_t *d_out, void *stream);
+/* prev_last: device uint32[2] from the previous rank (ignored when is_first); global_last:
+ * device uint32[2] from the last non-empty rank (becomes the context's last hash). */
+int kbz_shard_link(kbz_ctx_t *ctx, const uint32_t *prev_last, int is_first,
+                   const uint32_t *global_last, void *stream);
+int kbz_shard_reduce(kbz_ctx_t *ctx, void *stream);
+/* Copies this shard's OR aggregate (nclass*map_size bytes; nclass = 1 in DYNAMORIO mode,
+ * 3 otherwise) into device memory d_out. */
+int kbz_shard_aggregate(kbz_ctx_t *ctx, uint8_t *d_out, void *stream);
+size_t kbz_shard_aggregate_bytes(kbz_ctx_t *ctx);
+/* prefix/total: device, nclass*map_size bytes each (prefix may be NULL = all zero). */
+int kbz_shard_finish(kbz_ctx_t *ctx, const uint8_t *prefix, const uint8_t *total,
+                     uint8_t *hnb_out, void *stream);
+
+/* out[i] = OR of in[r*bytes + i] for r in [r_lo, r_hi).  Device, stream-ordered. */
+int kbz_or_reduce(uint8_t *out, const uint8_t *in, size_t r_lo, size_t r_hi, size_t bytes,
+                  void *stream);
+
+/* ---- merger -------------------------------------------------------------------------------- */
+/* out = AND of n states (state_bytes each, typically 3*map_size), row s at states +
+ * s*state_bytes.  n == 0 gives all-0xff.  Device, stream-ordered. */
+int kbz_merge_and_device(uint8_t *out, const uint8_t *states, size_t n, size_t state_bytes,
+                         void *stream);
+/* Host variant: streams host states (pageable or pinned) through the device. Synchronous. */
+int kbz_merge_and_host(uint8_t *out, const uint8_t *states, size_t n, size_t state_bytes);
+
+/* ---- standalone hashes over a batch --------------------------------------------------------- */
+/* h32_out[j] = hash32(row j, len, seed); x64_out[j] = XXH64(row j, len, seed).  len % 8 == 0
+ * for hash32 (afl_progs/hash.h:38); any len for XXH64.  Device, stream-ordered. */
+int kbz_hash32_device(const uint8_t *rows, size_t n, size_t stride, size_t len, uint32_t seed,
+                      uint32_t *h32_out, void *stream);
+int kbz_xxh64_device(const uint8_t *rows, size_t n, size_t stride, size_t len, uint64_t seed,
+                     uint64_t *x64_out, void *stream);
+
+/* Synchronise the context's work and report any device-side consistency error (-1). */
+int kbz_sync(kbz_ctx_t *ctx, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KBZ_TRIAGE_H */

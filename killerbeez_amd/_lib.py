@@ -1,0 +1,83 @@
+"""ctypes binding of libkbz_hip.so (include/kbz_triage.h).
+
+There is no fallback: if the HIP library is missing or cannot be loaded this module raises,
+so nothing can silently run a CPU path in its place.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+from . import build as _build
+
+_LIB = None
+
+# (name, restype, argtypes) for every function declared in include/kbz_triage.h
+_vp, _sz, _i, _u32, _u64 = C.c_void_p, C.c_size_t, C.c_int, C.c_uint32, C.c_uint64
+SIGNATURES = [
+    ("kbz_abi_version", _i, []),
+    ("kbz_last_error", C.c_char_p, []),
+    ("kbz_ctx_create", _vp, [_sz, _i, _sz]),
+    ("kbz_ctx_destroy", None, [_vp]),
+    ("kbz_set_ignore", _i, [_vp, _vp]),
+    ("kbz_get_virgin", _i, [_vp, _vp]),
+    ("kbz_set_virgin", _i, [_vp, _vp]),
+    ("kbz_get_last_hash", _i, [_vp, C.POINTER(_u32)]),
+    ("kbz_set_last_hash", _i, [_vp, _u32]),
+    ("kbz_virgin_device", _vp, [_vp]),
+    ("kbz_triage_batch_device", _i, [_vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _i, _vp]),
+    ("kbz_triage_batch_host", _i, [_vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _i]),
+    ("kbz_shard_begin", _i, [_vp, _vp, _sz, _sz, _vp, _vp, _vp, _i, _vp]),
+    ("kbz_shard_last_hash", _i, [_vp, _vp, _vp]),
+    ("kbz_shard_link", _i, [_vp, _vp, _i, _vp, _vp]),
+    ("kbz_shard_reduce", _i, [_vp, _vp]),
+    ("kbz_shard_aggregate", _i, [_vp, _vp, _vp]),
+    ("kbz_shard_aggregate_bytes", _sz, [_vp]),
+    ("kbz_shard_finish", _i, [_vp, _vp, _vp, _vp, _vp]),
+    ("kbz_or_reduce", _i, [_vp, _vp, _sz, _sz, _sz, _vp]),
+    ("kbz_merge_and_device", _i, [_vp, _vp, _sz, _sz, _vp]),
+    ("kbz_merge_and_host", _i, [_vp, _vp, _sz, _sz]),
+    ("kbz_hash32_device", _i, [_vp, _sz, _sz, _sz, _u32, _vp, _vp]),
+    ("kbz_xxh64_device", _i, [_vp, _sz, _sz, _sz, _u64, _vp, _vp]),
+    ("kbz_sync", _i, [_vp, _vp]),
+]
+
+
+def header_functions(header: str | None = None) -> list[str]:
+    """Names of the functions declared in include/kbz_triage.h."""
+    header = header or os.path.join(_build.INC, "kbz_triage.h")
+    text = open(header).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(kbz_[a-z0-9_]+)\s*\(", text)))
+
+
+class KbzError(RuntimeError):
+    pass
+
+
+def lib(build_if_missing: bool = True):
+    """Load libkbz_hip.so (building it first if needed and allowed)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = _build.HIP_LIB
+    if not os.path.exists(path):
+        if not build_if_missing:
+            raise KbzError(f"{path} not built (run killerbeez_amd.build.build_all())")
+        _build.build_hip()
+    L = C.CDLL(path)
+    for name, res, args in SIGNATURES:
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    if L.kbz_abi_version() != 1:
+        raise KbzError("ABI version mismatch")
+    _LIB = L
+    return L
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().kbz_last_error()
+        raise KbzError(f"{what}: {msg.decode() if msg else 'error'}")

@@ -1,0 +1,1177 @@
+// killerbeez_amd/csrc/kbz_triage.hip -- gfx950 coverage-triage engine behind include/kbz_triage.h.
+//
+// The reference checks every exec's trace against the virgin maps one at a time
+// (afl_instrumentation.c:600-662 has_new_bits inside finish_fuzz_round :231-274;
+// dynamorio_instrumentation.c:1428-1468 has_new_coverage).  Here a whole ordered batch is
+// triaged at once with the same results, using the per-byte decomposition of has_new_bits
+// (SURVEY.md §0.7): with P[j,i] the OR of traces k<j at byte i,
+//     trace j claims bits  t[j,i] & V[i] & ~P[j,i];
+//     hnb[j] = 2 if it claims anything where V[i]==0xff and P[j,i]==0, else 1 if it claims
+//              anything, else 0;                       V' = V & ~P[n,.]
+// Pipeline per batch (all stream-ordered, no host sync):
+//   pass1   one wave per 64-trace chunk streams its rows once through LDS (16 KiB tiles),
+//           lane = trace: transform (raw / classify / simplify), hash32 chain, optional XXH64,
+//           per-chunk column OR per virgin map, equality with the previous trace (DynamoRIO
+//           skip).  Word positions where every trace of the chunk is zero take a short path.
+//   skip    (DynamoRIO) skip[j] = hash[j]==hash[j-1]; chunks whose OR included a skipped
+//           trace that differs from its predecessor are recomputed without it (fixchunk).
+//   segor/total/prefix   OR of chunk aggregates per segment, exclusive prefix over segments,
+//           virgin update V' = V & ~OR_all.
+//   scan    per column, walk the segment's chunks: bits new to the chunk (OR_c & V & ~prefix)
+//           become claim items; each column yields at most 8 items per map per batch.
+//   resolve one wave per item re-reads that column of the claiming chunk's 64 rows and
+//           finds, per new bit, the first trace holding it -> atomicMax(hnb, 1 or 2).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kbz_device.h"
+#include "kbz_triage.h"
+
+using namespace kbz;
+
+namespace {
+
+constexpr int kChunk = 64;   // traces per chunk: one wave, one lane per trace
+constexpr int kTileW = 256;  // bytes of every row staged per tile
+constexpr int kTileWords = kTileW / 8;
+constexpr int kMaxSeg = 64;  // chunk segments for the column scan
+constexpr int kItemsPerCol = 8;
+
+enum { XF_RAW = 0, XF_CLASSIFY = 1, XF_SIMPLIFY = 2 };
+
+__host__ __device__ __forceinline__ int mode_nclass(int mode) {
+  return mode == KBZ_MODE_DYNAMORIO ? 1 : 3;
+}
+__host__ __device__ __forceinline__ int class_of(int mode, int outcome) {
+  if (mode == KBZ_MODE_DYNAMORIO) return 0;
+  return (outcome == KBZ_FUZZ_HANG) ? 1 : (outcome == KBZ_FUZZ_CRASH) ? 2 : 0;
+}
+// transform applied to traces of virgin class k
+__host__ __device__ __forceinline__ int class_xf(int mode, int k) {
+  if (mode == KBZ_MODE_DYNAMORIO) return XF_CLASSIFY;
+  if (k != 0) return XF_SIMPLIFY;
+  return mode == KBZ_MODE_AFL_CLASSIFY ? XF_CLASSIFY : XF_RAW;
+}
+
+__device__ __forceinline__ uint64_t xform8(uint64_t x, int xf) {
+  if (xf == XF_CLASSIFY) return classify8(x);
+  if (xf == XF_SIMPLIFY) return simplify8(x);
+  return x;
+}
+
+// OR of a 32-bit value over the 64 lanes of the wave (DPP row shifts + row broadcasts).
+__device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
+  return (uint64_t)wave_or32((uint32_t)v) | ((uint64_t)wave_or32((uint32_t)(v >> 32)) << 32);
+}
+// value of lane-1 (lane 0 gets 0)
+__device__ __forceinline__ uint64_t from_prev_lane(uint64_t v) {
+  const uint32_t lo = __shfl_up((uint32_t)v, 1), hi = __shfl_up((uint32_t)(v >> 32), 1);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ uint64_t ld_u64(const uint4 &v, int e) {
+  return e ? ((uint64_t)v.z | ((uint64_t)v.w << 32)) : ((uint64_t)v.x | ((uint64_t)v.y << 32));
+}
+__device__ __forceinline__ uint4 or4(uint4 a, uint4 b) {
+  return make_uint4(a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w);
+}
+__device__ __forceinline__ uint4 classify16(uint4 a) {
+  return make_uint4(classify4(a.x), classify4(a.y), classify4(a.z), classify4(a.w));
+}
+__device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
+  if (xf == XF_CLASSIFY) return classify4(b) & 0xff;
+  if (xf == XF_SIMPLIFY) return b ? 0x80u : 0x01u;
+  return b;
+}
+
+struct Pass1Args {
+  const uint8_t *traces;
+  size_t stride;
+  uint32_t n;
+  uint32_t map_size;
+  const int8_t *outcome;
+  const uint8_t *ignore;
+  uint32_t *h32;        // internal [n]
+  uint64_t *x64;        // user [n] or null
+  uint8_t *neq;         // [n]: transformed trace differs from the previous one (relevant bytes)
+  uint8_t *chunk_or;    // [chunks][nclass][map_size]
+  uint8_t *chunk_cls;   // [chunks] bitmask of classes present
+  uint32_t *shard_last; // [2]
+};
+
+// ---------------------------------------------------------------------------------------------
+// pass 1: one wave per chunk of 64 consecutive traces, lane = trace.
+// LDS tile = 64 rows x 256 B; 16-B slot q of row r lives at slot q ^ (r & 15) so both the
+// coalesced fill (4 rows per wave-instruction) and the row-per-lane ds_read_b128 are
+// conflict-free.
+// ---------------------------------------------------------------------------------------------
+template <int MODE, bool IGN, bool X64>
+__global__ __launch_bounds__(64) void k_pass1(Pass1Args a) {
+  constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
+  __shared__ uint4 lds[kChunk * kTileW / 16];
+  const int lane = threadIdx.x;
+  const uint32_t chunk = blockIdx.x;
+  const uint64_t row0 = (uint64_t)chunk * kChunk;
+  const int nrows = (int)min((uint64_t)kChunk, (uint64_t)a.n - row0);
+  const bool valid = lane < nrows;
+  const int oc = (valid && a.outcome) ? a.outcome[row0 + lane] : KBZ_FUZZ_NONE;
+  const int cls = class_of(MODE, oc);
+  const int xf = valid ? class_xf(MODE, cls) : XF_RAW;
+  const bool simp = (xf == XF_SIMPLIFY);
+  uint64_t present[NC];
+#pragma unroll
+  for (int k = 0; k < NC; k++) present[k] = __ballot(valid && cls == k);
+  if (lane == 0) {
+    uint8_t m = 0;
+#pragma unroll
+    for (int k = 0; k < NC; k++) m |= present[k] ? (1u << k) : 0u;
+    a.chunk_cls[chunk] = m;
+  }
+
+  const uint8_t *base = a.traces + row0 * a.stride;
+  const int lr = lane >> 4, ls = lane & 15;
+  const uint32_t ntiles = a.map_size / kTileW;
+  uint4 buf[16];
+  auto load_tile = [&](uint32_t t) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int r = 4 * i + lr;
+      if (r < nrows)
+        buf[i] = *(const uint4 *)(base + (size_t)r * a.stride + (size_t)t * kTileW + ls * 16);
+      else
+        buf[i] = make_uint4(0, 0, 0, 0);
+    }
+  };
+
+  uint64_t h = (uint64_t)(kHashConst ^ a.map_size);
+  uint64_t x0 = kXP1 + kXP2, x1 = kXP2, x2 = 0, x3 = 0 - kXP1;  // XXH64 lanes, seed 0
+  uint64_t neq = 0;
+  const uint64_t ksimp = h32_mix(kSimpleZero);
+
+  load_tile(0);
+  for (uint32_t t = 0; t < ntiles; t++) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int r = 4 * i + lr;
+      lds[r * 16 + (ls ^ (r & 15))] = buf[i];
+    }
+    __syncthreads();
+    if (t + 1 < ntiles) load_tile(t + 1);
+
+    const uint64_t *ig = IGN ? (const uint64_t *)(a.ignore + (size_t)t * kTileW) : nullptr;
+    uint64_t orw[NC];
+#pragma unroll
+    for (int k = 0; k < NC; k++) orw[k] = 0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      const uint4 v = lds[lane * 16 + (q ^ (lane & 15))];
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const int wi = 2 * q + e;
+        const uint64_t x = ld_u64(v, e);
+        uint64_t tw, kw;
+        if (__ballot(x != 0)) {
+          tw = xform8(x, xf);
+          const uint64_t ignw = IGN ? ig[wi] : ~0ull;
+          kw = h32_mix(tw & ignw);
+#pragma unroll
+          for (int k = 0; k < NC; k++) {
+            if (present[k]) {
+              const uint64_t r = wave_or64((valid && cls == k) ? tw : 0);
+              orw[k] = (lane == wi) ? r : orw[k];
+            }
+          }
+          if (MODE == KBZ_MODE_DYNAMORIO) {
+            const uint64_t rel = IGN ? ~nonzero_bytes8(ignw) : ~0ull;
+            neq |= (tw ^ from_prev_lane(tw)) & rel;
+          }
+        } else {
+          tw = simp ? kSimpleZero : 0;
+          kw = simp ? ksimp : 0;
+#pragma unroll
+          for (int k = 1; k < NC; k++)  // simplified classes see 0x01 bytes everywhere
+            if (present[k]) orw[k] = (lane == wi) ? kSimpleZero : orw[k];
+        }
+        h = h32_step(h, kw);
+        if (X64) {
+          if ((wi & 3) == 0) x0 = xx_round(x0, tw);
+          else if ((wi & 3) == 1) x1 = xx_round(x1, tw);
+          else if ((wi & 3) == 2) x2 = xx_round(x2, tw);
+          else x3 = xx_round(x3, tw);
+        }
+      }
+    }
+    if (lane < kTileWords) {
+#pragma unroll
+      for (int k = 0; k < NC; k++)
+        if (present[k])
+          *(uint64_t *)(a.chunk_or + ((size_t)chunk * NC + k) * a.map_size + (size_t)t * kTileW +
+                        lane * 8) = orw[k];
+    }
+    __syncthreads();
+  }
+
+  if (valid) {
+    const uint32_t h32 = h32_final(h);
+    a.h32[row0 + lane] = h32;
+    if (MODE == KBZ_MODE_DYNAMORIO) a.neq[row0 + lane] = neq != 0;
+    if (X64 && a.x64) {
+      uint64_t xh = rotl64(x0, 1) + rotl64(x1, 7) + rotl64(x2, 12) + rotl64(x3, 18);
+      xh = xx_merge(xh, x0);
+      xh = xx_merge(xh, x1);
+      xh = xx_merge(xh, x2);
+      xh = xx_merge(xh, x3);
+      xh += a.map_size;
+      a.x64[row0 + lane] = xx_avalanche(xh);
+    }
+    if (row0 + lane == (uint64_t)a.n - 1) {
+      a.shard_last[0] = h32;
+      a.shard_last[1] = 1;
+    }
+  }
+}
+
+// DynamoRIO last-hash skip: skip[j] = hash[j] == hash[j-1] (hash[-1] = previous exec's).
+// A skipped trace must not touch the virgin map; pass 1 OR'ed it in, which is harmless only
+// when it equals its predecessor on the bytes has_new_bits looks at.  Otherwise its chunk is
+// flagged for recomputation.
+__global__ void k_skip(const uint32_t *h32, const uint8_t *neq, uint32_t n,
+                       const uint32_t *prev_last /*[2] or null*/, const uint32_t *ctx_last,
+                       const uint32_t *global_last /*[2]*/, uint32_t *next_last,
+                       uint8_t *skip, uint8_t *flags) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j == 0) {
+    *next_last = global_last[1] ? global_last[0] : *ctx_last;
+  }
+  if (j >= n) return;
+  uint32_t hp;
+  if (j) hp = h32[j - 1];
+  else hp = prev_last ? prev_last[0] : *ctx_last;
+  const bool sk = h32[j] == hp;
+  skip[j] = sk;
+  if (sk && ((j % kChunk) == 0 || neq[j])) flags[j / kChunk] = 1;
+}
+
+// Recompute chunk ORs (DynamoRIO class 0) without skipped traces for flagged chunks.
+__global__ __launch_bounds__(256) void k_fixchunk(const uint8_t *traces, size_t stride, uint32_t n,
+                                                   uint32_t map_size, const uint8_t *skip,
+                                                   const uint8_t *flags, uint8_t *chunk_or) {
+  const uint32_t chunk = blockIdx.y;
+  if (!flags[chunk]) return;
+  const uint32_t col = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (col >= map_size) return;
+  const uint64_t row0 = (uint64_t)chunk * kChunk;
+  const int nrows = (int)min((uint64_t)kChunk, (uint64_t)n - row0);
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  for (int r = 0; r < nrows; r++) {
+    if (skip[row0 + r]) continue;
+    acc = or4(acc, classify16(*(const uint4 *)(traces + (row0 + r) * stride + col)));
+  }
+  *(uint4 *)(chunk_or + (size_t)chunk * map_size + col) = acc;
+}
+
+// segOR[s][k][:] = OR of chunk aggregates in segment s.
+__global__ __launch_bounds__(256) void k_segor(const uint8_t *chunk_or, const uint8_t *chunk_cls,
+                                                uint32_t nchunks, uint32_t seg_len, int nclass,
+                                                uint32_t map_size, uint8_t *segor) {
+  const uint32_t col = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  const uint32_t s = blockIdx.y;
+  const int k = blockIdx.z;
+  if (col >= map_size) return;
+  const uint32_t c0 = s * seg_len, c1 = min(nchunks, c0 + seg_len);
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  for (uint32_t c = c0; c < c1; c++)
+    if ((chunk_cls[c] >> k) & 1)
+      acc = or4(acc, *(const uint4 *)(chunk_or + ((size_t)c * nclass + k) * map_size + col));
+  *(uint4 *)(segor + ((size_t)s * nclass + k) * map_size + col) = acc;
+}
+
+// total[k][:] = OR over segments.
+__global__ __launch_bounds__(256) void k_total(const uint8_t *segor, uint32_t nseg, int nclass,
+                                                uint32_t map_size, uint8_t *total) {
+  const uint32_t col = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  const int k = blockIdx.z;
+  if (col >= map_size) return;
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  for (uint32_t s = 0; s < nseg; s++)
+    acc = or4(acc, *(const uint4 *)(segor + ((size_t)s * nclass + k) * map_size + col));
+  *(uint4 *)(total + (size_t)k * map_size + col) = acc;
+}
+
+// segprev = exclusive prefix over segments (seeded with the OR of earlier shards);
+// vnext = V & ~(OR of the whole batch) on the bytes has_new_bits may update.
+__global__ __launch_bounds__(256) void k_prefix(const uint8_t *segor, uint32_t nseg, int nclass,
+                                                 uint32_t map_size, const uint8_t *gprefix,
+                                                 const uint8_t *gtotal, const uint8_t *ignore,
+                                                 const uint8_t *vcur, uint8_t *vnext,
+                                                 uint8_t *segprev) {
+  const uint32_t col = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  const int k = blockIdx.z;
+  if (col >= map_size) return;
+  uint4 acc = gprefix ? *(const uint4 *)(gprefix + (size_t)k * map_size + col)
+                      : make_uint4(0, 0, 0, 0);
+  for (uint32_t s = 0; s < nseg; s++) {
+    *(uint4 *)(segprev + ((size_t)s * nclass + k) * map_size + col) = acc;
+    acc = or4(acc, *(const uint4 *)(segor + ((size_t)s * nclass + k) * map_size + col));
+  }
+  uint4 tot = *(const uint4 *)(gtotal + (size_t)k * map_size + col);
+  if (ignore) {  // has_new_bits_with_ignore never writes bytes whose ignore byte is nonzero
+    const uint4 ig = *(const uint4 *)(ignore + col);
+    const uint64_t m0 = nonzero_bytes8((uint64_t)ig.x | ((uint64_t)ig.y << 32));
+    const uint64_t m1 = nonzero_bytes8((uint64_t)ig.z | ((uint64_t)ig.w << 32));
+    tot.x &= ~(uint32_t)m0; tot.y &= ~(uint32_t)(m0 >> 32);
+    tot.z &= ~(uint32_t)m1; tot.w &= ~(uint32_t)(m1 >> 32);
+  }
+  const uint4 v = *(const uint4 *)(vcur + (size_t)k * map_size + col);
+  *(uint4 *)(vnext + (size_t)k * map_size + col) =
+      make_uint4(v.x & ~tot.x, v.y & ~tot.y, v.z & ~tot.z, v.w & ~tot.w);
+}
+
+// item: [7:0] new bits, [8] score-2 candidate, [10:9] class, [34:11] column, [63:35] chunk
+__device__ __forceinline__ uint64_t pack_item(uint32_t chunk, int k, uint32_t col, uint32_t nb,
+                                              bool f2) {
+  return ((uint64_t)chunk << 35) | ((uint64_t)col << 11) | ((uint64_t)k << 9) |
+         ((uint64_t)f2 << 8) | nb;
+}
+
+__global__ __launch_bounds__(256) void k_scan(const uint8_t *chunk_or, const uint8_t *chunk_cls,
+                                               uint32_t nchunks, uint32_t seg_len, int nclass,
+                                               uint32_t map_size, const uint8_t *segprev,
+                                               const uint8_t *vcur, const uint8_t *ignore,
+                                               uint64_t *items, uint32_t cap, uint32_t *counters) {
+  const uint32_t col = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  const uint32_t s = blockIdx.y;
+  const int k = blockIdx.z;
+  if (col >= map_size) return;
+  const uint32_t c0 = s * seg_len, c1 = min(nchunks, c0 + seg_len);
+  uint8_t prev[16], vir[16], rel[16];
+  {
+    const uint4 p = *(const uint4 *)(segprev + ((size_t)s * nclass + k) * map_size + col);
+    const uint4 v = *(const uint4 *)(vcur + (size_t)k * map_size + col);
+    memcpy(prev, &p, 16);
+    memcpy(vir, &v, 16);
+    if (ignore) {
+      const uint4 ig = *(const uint4 *)(ignore + col);
+      uint8_t igb[16];
+      memcpy(igb, &ig, 16);
+      for (int b = 0; b < 16; b++) rel[b] = igb[b] ? 0 : 0xff;
+    } else {
+      for (int b = 0; b < 16; b++) rel[b] = 0xff;
+    }
+  }
+  for (uint32_t c = c0; c < c1; c++) {
+    if (!((chunk_cls[c] >> k) & 1)) continue;
+    const uint4 o4 = *(const uint4 *)(chunk_or + ((size_t)c * nclass + k) * map_size + col);
+    uint8_t o[16];
+    memcpy(o, &o4, 16);
+    for (int b = 0; b < 16; b++) {
+      const uint32_t nb = o[b] & vir[b] & (uint8_t)~prev[b] & rel[b];
+      if (nb) {
+        const uint32_t idx = atomicAdd(&counters[0], 1u);
+        if (idx < cap) items[idx] = pack_item(c, k, col + b, nb, vir[b] == 0xff && prev[b] == 0);
+        else atomicOr(&counters[1], 1u);
+      }
+      prev[b] |= o[b];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_resolve(const uint8_t *traces, size_t stride, uint32_t n,
+                                                  int mode, const int8_t *outcome,
+                                                  const uint8_t *skip, const uint64_t *items,
+                                                  const uint32_t *counters, uint32_t cap,
+                                                  uint32_t *hnb32, uint32_t *err) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t cnt = min(counters[0], cap);
+  for (uint32_t it = wave; it < cnt; it += nwaves) {
+    const uint64_t item = items[it];
+    const uint32_t nb = item & 0xff;
+    const bool f2 = (item >> 8) & 1;
+    const int k = (item >> 9) & 3;
+    const uint32_t col = (item >> 11) & 0xffffff;
+    const uint32_t chunk = (uint32_t)(item >> 35);
+    const uint64_t row = (uint64_t)chunk * kChunk + lane;
+    bool ok = row < n;
+    if (ok) {
+      const int oc = outcome ? outcome[row] : KBZ_FUZZ_NONE;
+      ok = class_of(mode, oc) == k;
+      if (ok && skip) ok = !skip[row];
+    }
+    const uint32_t tb = ok ? byte_xform(traces[row * stride + col], class_xf(mode, k)) : 0u;
+    const uint64_t first_nz = __ballot(tb != 0);
+    uint64_t claimers = 0;
+    for (int b = 0; b < 8; b++) {
+      if ((nb >> b) & 1) {
+        const uint64_t m = __ballot((tb >> b) & 1);
+        if (!m) {
+          if (lane == 0) atomicOr(err, 2u);
+        }
+        claimers |= m & (0 - m);
+      }
+    }
+    if ((claimers >> lane) & 1) {
+      const bool two = f2 && first_nz && (lane == __builtin_ctzll(first_nz));
+      atomicMax(&hnb32[row], two ? 2u : 1u);
+    }
+  }
+}
+
+__global__ void k_pack(const uint32_t *hnb32, const uint32_t *h32, uint32_t n, uint8_t *hnb_out,
+                       uint32_t *h32_out) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  hnb_out[j] = (uint8_t)hnb32[j];
+  if (h32_out) h32_out[j] = h32[j];
+}
+
+__global__ __launch_bounds__(256) void k_or_reduce(uint8_t *out, const uint8_t *in, size_t r_lo,
+                                                    size_t r_hi, size_t bytes) {
+  const size_t i = (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (i + 16 <= bytes) {
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (size_t r = r_lo; r < r_hi; r++) acc = or4(acc, *(const uint4 *)(in + r * bytes + i));
+    *(uint4 *)(out + i) = acc;
+  } else {
+    for (size_t b = i; b < bytes; b++) {
+      uint8_t acc = 0;
+      for (size_t r = r_lo; r < r_hi; r++) acc |= in[r * bytes + b];
+      out[b] = acc;
+    }
+  }
+}
+
+// ---- merger: AND-fold -----------------------------------------------------------------------
+// partial[g][:] = AND of states in group g (16 B per thread, 4 independent loads in flight).
+__global__ __launch_bounds__(256) void k_and_groups(const uint8_t *states, size_t n,
+                                                     size_t state_bytes, size_t group_len,
+                                                     uint8_t *partial) {
+  const size_t col = (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  const size_t g = blockIdx.y;
+  if (col >= state_bytes) return;
+  const size_t s0 = g * group_len, s1 = std::min(n, s0 + group_len);
+  uint4 acc = make_uint4(~0u, ~0u, ~0u, ~0u);
+  size_t s = s0;
+  for (; s + 4 <= s1; s += 4) {
+    const uint4 a = *(const uint4 *)(states + s * state_bytes + col);
+    const uint4 b = *(const uint4 *)(states + (s + 1) * state_bytes + col);
+    const uint4 c = *(const uint4 *)(states + (s + 2) * state_bytes + col);
+    const uint4 d = *(const uint4 *)(states + (s + 3) * state_bytes + col);
+    acc.x &= a.x & b.x & c.x & d.x;
+    acc.y &= a.y & b.y & c.y & d.y;
+    acc.z &= a.z & b.z & c.z & d.z;
+    acc.w &= a.w & b.w & c.w & d.w;
+  }
+  for (; s < s1; s++) {
+    const uint4 a = *(const uint4 *)(states + s * state_bytes + col);
+    acc.x &= a.x; acc.y &= a.y; acc.z &= a.z; acc.w &= a.w;
+  }
+  *(uint4 *)(partial + g * state_bytes + col) = acc;
+}
+__global__ __launch_bounds__(256) void k_and_rows(const uint8_t *rows, size_t nrows, size_t bytes,
+                                                   uint8_t *out, int accumulate) {
+  const size_t col = (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (col >= bytes) return;
+  uint4 acc = accumulate ? *(const uint4 *)(out + col) : make_uint4(~0u, ~0u, ~0u, ~0u);
+  for (size_t r = 0; r < nrows; r++) {
+    const uint4 a = *(const uint4 *)(rows + r * bytes + col);
+    acc.x &= a.x; acc.y &= a.y; acc.z &= a.z; acc.w &= a.w;
+  }
+  *(uint4 *)(out + col) = acc;
+}
+// byte-granular fallback for state sizes that are not a multiple of 16
+__global__ void k_and_bytes(const uint8_t *states, size_t n, size_t state_bytes, uint8_t *out,
+                            int accumulate) {
+  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= state_bytes) return;
+  uint8_t acc = accumulate ? out[b] : 0xff;
+  for (size_t s = 0; s < n; s++) acc &= states[s * state_bytes + b];
+  out[b] = acc;
+}
+
+// ---- standalone row hashes (utility path: one lane per row, direct loads) ---------------------
+__global__ void k_rowhash32(const uint8_t *rows, size_t n, size_t stride, size_t len, uint32_t seed,
+                            uint32_t *out) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint8_t *p = rows + j * stride;
+  uint64_t h = (uint64_t)(seed ^ (uint32_t)len);
+  for (size_t w = 0; w < len / 8; w++) {
+    uint64_t k;
+    memcpy(&k, p + 8 * w, 8);
+    h = h32_step(h, h32_mix(k));
+  }
+  out[j] = h32_final(h);
+}
+__global__ void k_rowxxh64(const uint8_t *rows, size_t n, size_t stride, size_t len, uint64_t seed,
+                           uint64_t *out) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint8_t *p = rows + j * stride, *end = p + len;
+  uint64_t h;
+  if (len >= 32) {
+    uint64_t a = seed + kXP1 + kXP2, b = seed + kXP2, c = seed, d = seed - kXP1;
+    while (p + 32 <= end) {
+      uint64_t w[4];
+      memcpy(w, p, 32);
+      a = xx_round(a, w[0]);
+      b = xx_round(b, w[1]);
+      c = xx_round(c, w[2]);
+      d = xx_round(d, w[3]);
+      p += 32;
+    }
+    h = rotl64(a, 1) + rotl64(b, 7) + rotl64(c, 12) + rotl64(d, 18);
+    h = xx_merge(h, a);
+    h = xx_merge(h, b);
+    h = xx_merge(h, c);
+    h = xx_merge(h, d);
+  } else {
+    h = seed + kXP5;
+  }
+  h += (uint64_t)len;
+  while (p + 8 <= end) {
+    uint64_t w;
+    memcpy(&w, p, 8);
+    h ^= xx_round(0, w);
+    h = rotl64(h, 27) * kXP1 + kXP4;
+    p += 8;
+  }
+  if (p + 4 <= end) {
+    uint32_t w;
+    memcpy(&w, p, 4);
+    h ^= (uint64_t)w * kXP1;
+    h = rotl64(h, 23) * kXP2 + kXP3;
+    p += 4;
+  }
+  while (p < end) {
+    h ^= (*p) * kXP5;
+    h = rotl64(h, 11) * kXP1;
+    p++;
+  }
+  out[j] = xx_avalanche(h);
+}
+
+}  // namespace
+
+// =============================================================================================
+// host runtime
+// =============================================================================================
+struct kbz_ctx {
+  int device = 0;
+  size_t M = 0;
+  int mode = 0;
+  int nc = 1;
+  size_t max_batch = 0;
+  size_t max_chunks = 0;
+  uint8_t *V[2] = {nullptr, nullptr};
+  int vcur = 0;
+  uint32_t *last = nullptr;  // [2] double-buffered last hash
+  int lcur = 0;
+  uint8_t *ignore = nullptr;
+  uint8_t *chunk_or = nullptr;
+  uint8_t *chunk_cls = nullptr;
+  uint8_t *flags = nullptr;
+  uint8_t *skip = nullptr;
+  uint8_t *neq = nullptr;
+  uint32_t *h32 = nullptr;
+  uint32_t *hnb32 = nullptr;
+  uint8_t *segor = nullptr;
+  uint8_t *segprev = nullptr;
+  uint8_t *total = nullptr;
+  uint64_t *items = nullptr;
+  uint32_t item_cap = 0;
+  uint32_t *counters = nullptr;  // [0] items, [1] overflow, [2] resolve error
+  uint32_t *shard_last = nullptr;  // [2]
+  // in-flight shard
+  const uint8_t *cur_traces = nullptr;
+  size_t cur_n = 0, cur_stride = 0;
+  const int8_t *cur_outcome = nullptr;
+  uint32_t *cur_h32_out = nullptr;
+  uint32_t cur_chunks = 0, cur_seg_len = 1, cur_nseg = 1;
+  int stage = 0;
+  // host streaming
+  hipStream_t copy_stream = nullptr, work_stream = nullptr;
+  uint8_t *pin[2] = {nullptr, nullptr};
+  int8_t *pin_oc[2] = {nullptr, nullptr};
+  uint8_t *dslot[2] = {nullptr, nullptr};
+  int8_t *dslot_oc[2] = {nullptr, nullptr};
+  uint8_t *dres_hnb = nullptr;
+  uint32_t *dres_h32 = nullptr;
+  uint64_t *dres_x64 = nullptr;
+  size_t slot_rows = 0;
+  hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_used[2] = {nullptr, nullptr};
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(const std::string &msg) {
+  g_err = msg;
+  return -1;
+}
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      return fail(std::string(#expr) + ": " + hipGetErrorString(_e));                   \
+  } while (0)
+
+struct DevGuard {
+  int old = -1;
+  explicit DevGuard(int dev) {
+    (void)hipGetDevice(&old);
+    if (old != dev) (void)hipSetDevice(dev);
+  }
+  ~DevGuard() {
+    int cur;
+    (void)hipGetDevice(&cur);
+    if (old >= 0 && cur != old) (void)hipSetDevice(old);
+  }
+};
+
+inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+
+template <typename T>
+int dalloc(T **p, size_t count) {
+  if (count == 0) count = 1;
+  HIP_TRY(hipMalloc((void **)p, count * sizeof(T)));
+  return 0;
+}
+
+void free_ctx(kbz_ctx *c) {
+  if (!c) return;
+  DevGuard g(c->device);
+  void *ptrs[] = {c->V[0], c->V[1], c->last, c->ignore, c->chunk_or, c->chunk_cls, c->flags,
+                  c->skip, c->neq, c->h32, c->hnb32, c->segor, c->segprev, c->total,
+                  c->items, c->counters, c->shard_last, c->dslot[0], c->dslot[1],
+                  c->dslot_oc[0], c->dslot_oc[1], c->dres_hnb, c->dres_h32, c->dres_x64};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  for (int i = 0; i < 2; i++) {
+    if (c->pin[i]) (void)hipHostFree(c->pin[i]);
+    if (c->pin_oc[i]) (void)hipHostFree(c->pin_oc[i]);
+    if (c->ev_copied[i]) (void)hipEventDestroy(c->ev_copied[i]);
+    if (c->ev_used[i]) (void)hipEventDestroy(c->ev_used[i]);
+  }
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+  if (c->work_stream) (void)hipStreamDestroy(c->work_stream);
+  delete c;
+}
+
+template <int MODE, bool IGN, bool X64>
+void launch_pass1(const Pass1Args &a, uint32_t chunks, hipStream_t s) {
+  hipLaunchKernelGGL((k_pass1<MODE, IGN, X64>), dim3(chunks), dim3(64), 0, s, a);
+}
+
+int pass1_dispatch(kbz_ctx *c, const Pass1Args &a, uint32_t chunks, bool x64, hipStream_t s) {
+  const bool ign = c->ignore != nullptr && c->mode == KBZ_MODE_DYNAMORIO;
+  switch (c->mode) {
+    case KBZ_MODE_AFL:
+      x64 ? launch_pass1<KBZ_MODE_AFL, false, true>(a, chunks, s)
+          : launch_pass1<KBZ_MODE_AFL, false, false>(a, chunks, s);
+      break;
+    case KBZ_MODE_AFL_CLASSIFY:
+      x64 ? launch_pass1<KBZ_MODE_AFL_CLASSIFY, false, true>(a, chunks, s)
+          : launch_pass1<KBZ_MODE_AFL_CLASSIFY, false, false>(a, chunks, s);
+      break;
+    default:
+      if (ign)
+        x64 ? launch_pass1<KBZ_MODE_DYNAMORIO, true, true>(a, chunks, s)
+            : launch_pass1<KBZ_MODE_DYNAMORIO, true, false>(a, chunks, s);
+      else
+        x64 ? launch_pass1<KBZ_MODE_DYNAMORIO, false, true>(a, chunks, s)
+            : launch_pass1<KBZ_MODE_DYNAMORIO, false, false>(a, chunks, s);
+  }
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int check_rows(const void *p, size_t stride, size_t M) {
+  if (((uintptr_t)p & 15) || (stride & 15) || stride < M)
+    return fail("traces must be 16-byte aligned with stride % 16 == 0 and stride >= map_size");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kbz_abi_version(void) { return KBZ_ABI_VERSION; }
+const char *kbz_last_error(void) { return g_err.c_str(); }
+
+kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
+  if (map_size < kTileW || map_size % kTileW || map_size > (1u << 24)) {
+    fail("map_size must be a multiple of 256 in [256, 16 MiB]");
+    return nullptr;
+  }
+  if (mode < 0 || mode > 2) {
+    fail("bad mode");
+    return nullptr;
+  }
+  if (max_batch == 0 || max_batch > (1ull << 31)) {
+    fail("max_batch must be in [1, 2^31]");
+    return nullptr;
+  }
+  kbz_ctx *c = new kbz_ctx();
+  (void)hipGetDevice(&c->device);
+  c->M = map_size;
+  c->mode = mode;
+  c->nc = mode_nclass(mode);
+  c->max_batch = max_batch;
+  c->max_chunks = cdiv(max_batch, kChunk);
+  const size_t M = map_size, nc = c->nc;
+  c->item_cap = (uint32_t)std::min<size_t>(kItemsPerCol * M * nc + 1024, 0xffffffffu);
+  bool ok = !dalloc(&c->V[0], 3 * M) && !dalloc(&c->V[1], 3 * M) && !dalloc(&c->last, 2) &&
+            !dalloc(&c->chunk_or, c->max_chunks * nc * M) && !dalloc(&c->chunk_cls, c->max_chunks) &&
+            !dalloc(&c->flags, c->max_chunks) && !dalloc(&c->skip, max_batch) &&
+            !dalloc(&c->neq, max_batch) && !dalloc(&c->h32, max_batch) &&
+            !dalloc(&c->hnb32, max_batch) && !dalloc(&c->segor, kMaxSeg * nc * M) &&
+            !dalloc(&c->segprev, kMaxSeg * nc * M) && !dalloc(&c->total, nc * M) &&
+            !dalloc(&c->items, c->item_cap) && !dalloc(&c->counters, 4) &&
+            !dalloc(&c->shard_last, 2);
+  if (!ok) {
+    std::string e = g_err;
+    free_ctx(c);
+    g_err = e;
+    return nullptr;
+  }
+  (void)hipMemset(c->V[0], 0xff, 3 * M);
+  (void)hipMemset(c->last, 0, 2 * sizeof(uint32_t));
+  (void)hipMemset(c->counters, 0, 4 * sizeof(uint32_t));
+  if (hipDeviceSynchronize() != hipSuccess) {
+    fail("device init failed");
+    free_ctx(c);
+    return nullptr;
+  }
+  return c;
+}
+
+void kbz_ctx_destroy(kbz_ctx_t *ctx) { free_ctx(ctx); }
+
+int kbz_set_ignore(kbz_ctx_t *c, const uint8_t *host_ignore) {
+  if (!c) return fail("null ctx");
+  DevGuard g(c->device);
+  if (!host_ignore) {
+    if (c->ignore) (void)hipFree(c->ignore);
+    c->ignore = nullptr;
+    return 0;
+  }
+  if (!c->ignore && dalloc(&c->ignore, c->M)) return -1;
+  HIP_TRY(hipMemcpy(c->ignore, host_ignore, c->M, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int kbz_get_virgin(kbz_ctx_t *c, uint8_t *out) {
+  if (!c || !out) return fail("null argument");
+  DevGuard g(c->device);
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, c->V[c->vcur], 3 * c->M, hipMemcpyDeviceToHost));
+  return 0;
+}
+int kbz_set_virgin(kbz_ctx_t *c, const uint8_t *in) {
+  if (!c || !in) return fail("null argument");
+  DevGuard g(c->device);
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(c->V[c->vcur], in, 3 * c->M, hipMemcpyHostToDevice));
+  return 0;
+}
+int kbz_get_last_hash(kbz_ctx_t *c, uint32_t *out) {
+  if (!c || !out) return fail("null argument");
+  DevGuard g(c->device);
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, c->last + c->lcur, 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+int kbz_set_last_hash(kbz_ctx_t *c, uint32_t v) {
+  if (!c) return fail("null ctx");
+  DevGuard g(c->device);
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(c->last + c->lcur, &v, 4, hipMemcpyHostToDevice));
+  return 0;
+}
+uint8_t *kbz_virgin_device(kbz_ctx_t *c) { return c ? c->V[c->vcur] : nullptr; }
+
+int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride,
+                    const int8_t *outcome, uint32_t *h32_out, uint64_t *x64_out, int want,
+                    void *stream) {
+  if (!c) return fail("null ctx");
+  if (n > c->max_batch) return fail("n exceeds max_batch");
+  if (n && check_rows(traces, stride, c->M)) return -1;
+  DevGuard g(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  c->cur_traces = traces;
+  c->cur_n = n;
+  c->cur_stride = stride;
+  c->cur_outcome = outcome;
+  c->cur_h32_out = h32_out;
+  c->cur_chunks = cdiv(n, kChunk);
+  c->cur_nseg = std::max(1u, std::min<unsigned>(kMaxSeg, c->cur_chunks));
+  c->cur_seg_len = std::max(1u, cdiv(c->cur_chunks, c->cur_nseg));
+  c->cur_nseg = std::max(1u, cdiv(c->cur_chunks, c->cur_seg_len));
+  HIP_TRY(hipMemsetAsync(c->shard_last, 0, 2 * sizeof(uint32_t), s));
+  HIP_TRY(hipMemsetAsync(c->counters, 0, 4 * sizeof(uint32_t), s));
+  if (n == 0) {
+    c->stage = 1;
+    return 0;
+  }
+  HIP_TRY(hipMemsetAsync(c->hnb32, 0, n * sizeof(uint32_t), s));
+  Pass1Args a;
+  a.traces = traces;
+  a.stride = stride;
+  a.n = (uint32_t)n;
+  a.map_size = (uint32_t)c->M;
+  a.outcome = outcome;
+  a.ignore = c->ignore;
+  a.h32 = c->h32;
+  a.x64 = (want & KBZ_WANT_X64) ? x64_out : nullptr;
+  a.neq = c->neq;
+  a.chunk_or = c->chunk_or;
+  a.chunk_cls = c->chunk_cls;
+  a.shard_last = c->shard_last;
+  if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, s)) return -1;
+  c->stage = 1;
+  return 0;
+}
+
+int kbz_shard_last_hash(kbz_ctx_t *c, uint32_t *d_out, void *stream) {
+  if (!c || !d_out) return fail("null argument");
+  if (c->stage < 1) return fail("kbz_shard_last_hash: call kbz_shard_begin first");
+  DevGuard g(c->device);
+  HIP_TRY(hipMemcpyAsync(d_out, c->shard_last, 2 * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
+  return 0;
+}
+
+int kbz_shard_link(kbz_ctx_t *c, const uint32_t *prev_last, int is_first,
+                   const uint32_t *global_last, void *stream) {
+  if (!c || c->stage != 1) return fail("kbz_shard_link: call kbz_shard_begin first");
+  DevGuard g(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (c->mode == KBZ_MODE_DYNAMORIO) {
+    const size_t n = c->cur_n;
+    if (n) HIP_TRY(hipMemsetAsync(c->flags, 0, c->cur_chunks, s));
+    const int nl = c->lcur ^ 1;
+    hipLaunchKernelGGL(k_skip, dim3(std::max(1u, cdiv(n, 256))), dim3(256), 0, s, c->h32, c->neq,
+                       (uint32_t)n, is_first ? nullptr : prev_last, c->last + c->lcur,
+                       global_last ? global_last : c->shard_last, c->last + nl, c->skip,
+                       c->flags);
+    HIP_TRY(hipGetLastError());
+    c->lcur = nl;
+    if (n) {
+      hipLaunchKernelGGL(k_fixchunk, dim3(cdiv(c->M / 16, 256), c->cur_chunks), dim3(256), 0, s,
+                         c->cur_traces, c->cur_stride, (uint32_t)n, (uint32_t)c->M, c->skip,
+                         c->flags, c->chunk_or);
+      HIP_TRY(hipGetLastError());
+    }
+  }
+  c->stage = 2;
+  return 0;
+}
+
+int kbz_shard_reduce(kbz_ctx_t *c, void *stream) {
+  if (!c || c->stage != 2) return fail("kbz_shard_reduce: call kbz_shard_link first");
+  DevGuard g(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned gx = cdiv(c->M / 16, 256);
+  if (c->cur_n == 0) {
+    HIP_TRY(hipMemsetAsync(c->total, 0, c->nc * c->M, s));
+    HIP_TRY(hipMemsetAsync(c->segor, 0, c->nc * c->M, s));
+  } else {
+    hipLaunchKernelGGL(k_segor, dim3(gx, c->cur_nseg, c->nc), dim3(256), 0, s, c->chunk_or,
+                       c->chunk_cls, c->cur_chunks, c->cur_seg_len, c->nc, (uint32_t)c->M,
+                       c->segor);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_total, dim3(gx, 1, c->nc), dim3(256), 0, s, c->segor, c->cur_nseg,
+                       c->nc, (uint32_t)c->M, c->total);
+    HIP_TRY(hipGetLastError());
+  }
+  c->stage = 3;
+  return 0;
+}
+
+int kbz_shard_aggregate(kbz_ctx_t *c, uint8_t *d_out, void *stream) {
+  if (!c || !d_out) return fail("null argument");
+  if (c->stage != 3) return fail("kbz_shard_aggregate: call kbz_shard_reduce first");
+  DevGuard g(c->device);
+  HIP_TRY(hipMemcpyAsync(d_out, c->total, c->nc * c->M, hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
+  return 0;
+}
+size_t kbz_shard_aggregate_bytes(kbz_ctx_t *c) { return c ? c->nc * c->M : 0; }
+
+int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, uint8_t *hnb_out,
+                     void *stream) {
+  if (!c || c->stage != 3) return fail("kbz_shard_finish: call kbz_shard_reduce first");
+  if (!total) return fail("kbz_shard_finish: total is required");
+  DevGuard g(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned gx = cdiv(c->M / 16, 256);
+  const int vn = c->vcur ^ 1;
+  const uint8_t *ign = (c->mode == KBZ_MODE_DYNAMORIO) ? c->ignore : nullptr;
+  const uint32_t nseg = c->cur_n ? c->cur_nseg : 1;
+  hipLaunchKernelGGL(k_prefix, dim3(gx, 1, c->nc), dim3(256), 0, s, c->segor, nseg, c->nc,
+                     (uint32_t)c->M, prefix, total, ign, c->V[c->vcur], c->V[vn], c->segprev);
+  HIP_TRY(hipGetLastError());
+  if (c->nc < 3)  // DYNAMORIO: tmout/crash maps are carried unchanged
+    HIP_TRY(hipMemcpyAsync(c->V[vn] + c->nc * c->M, c->V[c->vcur] + c->nc * c->M,
+                           (3 - c->nc) * c->M, hipMemcpyDeviceToDevice, s));
+  if (c->cur_n) {
+    hipLaunchKernelGGL(k_scan, dim3(gx, c->cur_nseg, c->nc), dim3(256), 0, s, c->chunk_or,
+                       c->chunk_cls, c->cur_chunks, c->cur_seg_len, c->nc, (uint32_t)c->M,
+                       c->segprev, c->V[c->vcur], ign, c->items, c->item_cap, c->counters);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_resolve, dim3(512), dim3(256), 0, s, c->cur_traces, c->cur_stride,
+                       (uint32_t)c->cur_n, c->mode, c->cur_outcome,
+                       c->mode == KBZ_MODE_DYNAMORIO ? c->skip : nullptr, c->items, c->counters,
+                       c->item_cap, c->hnb32, c->counters + 2);
+    HIP_TRY(hipGetLastError());
+    if (hnb_out || c->cur_h32_out) {
+      if (hnb_out) {
+        hipLaunchKernelGGL(k_pack, dim3(cdiv(c->cur_n, 256)), dim3(256), 0, s, c->hnb32, c->h32,
+                           (uint32_t)c->cur_n, hnb_out, c->cur_h32_out);
+        HIP_TRY(hipGetLastError());
+      } else {
+        HIP_TRY(hipMemcpyAsync(c->cur_h32_out, c->h32, c->cur_n * 4, hipMemcpyDeviceToDevice, s));
+      }
+    }
+  }
+  c->vcur = vn;
+  c->stage = 0;
+  return 0;
+}
+
+int kbz_triage_batch_device(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride,
+                            const int8_t *outcome, uint8_t *hnb_out, uint32_t *h32_out,
+                            uint64_t *x64_out, int want, void *stream) {
+  if (kbz_shard_begin(c, traces, n, stride, outcome, h32_out, x64_out, want, stream)) return -1;
+  if (kbz_shard_link(c, nullptr, 1, nullptr, stream)) return -1;
+  if (kbz_shard_reduce(c, stream)) return -1;
+  return kbz_shard_finish(c, nullptr, c->total, hnb_out, stream);
+}
+
+int kbz_or_reduce(uint8_t *out, const uint8_t *in, size_t r_lo, size_t r_hi, size_t bytes,
+                  void *stream) {
+  if (!out || (!in && r_hi > r_lo)) return fail("null argument");
+  if (bytes == 0) return 0;
+  hipLaunchKernelGGL(k_or_reduce, dim3(cdiv(bytes, 16 * 256)), dim3(256), 0, (hipStream_t)stream,
+                     out, in, r_lo, r_hi, bytes);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int kbz_sync(kbz_ctx_t *c, void *stream) {
+  if (!c) return fail("null ctx");
+  DevGuard g(c->device);
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  uint32_t cnt[4];
+  HIP_TRY(hipMemcpy(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost));
+  if (cnt[1]) return fail("claim list overflow");
+  if (cnt[2]) return fail("inconsistent claim (internal error)");
+  return 0;
+}
+
+// ---- host streaming ---------------------------------------------------------------------------
+namespace {
+int ensure_streaming(kbz_ctx *c) {
+  if (c->work_stream) return 0;
+  // slot = up to 256 MiB of traces (>= 64 rows), bounded by max_batch
+  size_t rows = std::max<size_t>(64, (256u << 20) / c->M);
+  rows = std::min(rows, c->max_batch);
+  c->slot_rows = rows;
+  HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&c->work_stream, hipStreamNonBlocking));
+  for (int i = 0; i < 2; i++) {
+    HIP_TRY(hipHostMalloc((void **)&c->pin[i], rows * c->M, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void **)&c->pin_oc[i], rows, hipHostMallocDefault));
+    HIP_TRY(hipMalloc((void **)&c->dslot[i], rows * c->M));
+    HIP_TRY(hipMalloc((void **)&c->dslot_oc[i], rows));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_copied[i], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_used[i], hipEventDisableTiming));
+  }
+  HIP_TRY(hipMalloc((void **)&c->dres_hnb, c->max_batch));
+  HIP_TRY(hipMalloc((void **)&c->dres_h32, c->max_batch * 4));
+  HIP_TRY(hipMalloc((void **)&c->dres_x64, c->max_batch * 8));
+  return 0;
+}
+}  // namespace
+
+int kbz_triage_batch_host(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride,
+                          const int8_t *outcome, uint8_t *hnb_out, uint32_t *h32_out,
+                          uint64_t *x64_out, int want) {
+  if (!c) return fail("null ctx");
+  if (n > c->max_batch) return fail("n exceeds max_batch");
+  if (stride < c->M) return fail("stride < map_size");
+  DevGuard g(c->device);
+  if (ensure_streaming(c)) return -1;
+  const size_t R = c->slot_rows, M = c->M;
+  const size_t nsub = (n + R - 1) / R;
+  // sub-batches are triaged in order against the carried virgin state: the sequential
+  // semantics compose, so this equals one triage of the whole batch.
+  for (size_t b = 0; b < nsub; b++) {
+    const int sl = (int)(b & 1);
+    const size_t lo = b * R, cnt = std::min(R, n - lo);
+    HIP_TRY(hipEventSynchronize(c->ev_used[sl]));  // slot free (no-op the first time)
+    if (stride == M) {
+      memcpy(c->pin[sl], traces + lo * M, cnt * M);
+    } else {
+      for (size_t r = 0; r < cnt; r++) memcpy(c->pin[sl] + r * M, traces + (lo + r) * stride, M);
+    }
+    if (outcome) memcpy(c->pin_oc[sl], outcome + lo, cnt);
+    HIP_TRY(hipMemcpyAsync(c->dslot[sl], c->pin[sl], cnt * M, hipMemcpyHostToDevice,
+                           c->copy_stream));
+    if (outcome)
+      HIP_TRY(hipMemcpyAsync(c->dslot_oc[sl], c->pin_oc[sl], cnt, hipMemcpyHostToDevice,
+                             c->copy_stream));
+    HIP_TRY(hipEventRecord(c->ev_copied[sl], c->copy_stream));
+    HIP_TRY(hipStreamWaitEvent(c->work_stream, c->ev_copied[sl], 0));
+    if (kbz_triage_batch_device(c, c->dslot[sl], cnt, M, outcome ? c->dslot_oc[sl] : nullptr,
+                                c->dres_hnb + lo, h32_out ? c->dres_h32 + lo : nullptr,
+                                x64_out ? c->dres_x64 + lo : nullptr, want, c->work_stream))
+      return -1;
+    HIP_TRY(hipEventRecord(c->ev_used[sl], c->work_stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->work_stream));
+  if (n) {
+    if (hnb_out) HIP_TRY(hipMemcpy(hnb_out, c->dres_hnb, n, hipMemcpyDeviceToHost));
+    if (h32_out) HIP_TRY(hipMemcpy(h32_out, c->dres_h32, n * 4, hipMemcpyDeviceToHost));
+    if (x64_out && (want & KBZ_WANT_X64))
+      HIP_TRY(hipMemcpy(x64_out, c->dres_x64, n * 8, hipMemcpyDeviceToHost));
+  }
+  return kbz_sync(c, c->work_stream);
+}
+
+// ---- merger -----------------------------------------------------------------------------------
+int kbz_merge_and_device(uint8_t *out, const uint8_t *states, size_t n, size_t state_bytes,
+                         void *stream) {
+  if (!out || (!states && n)) return fail("null argument");
+  if (state_bytes == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) {
+    HIP_TRY(hipMemsetAsync(out, 0xff, state_bytes, s));
+    return 0;
+  }
+  if ((state_bytes & 15) || ((uintptr_t)states & 15) || ((uintptr_t)out & 15)) {
+    hipLaunchKernelGGL(k_and_bytes, dim3(cdiv(state_bytes, 256)), dim3(256), 0, s, states, n,
+                       state_bytes, out, 0);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+  const unsigned gx = cdiv(state_bytes / 16, 256);
+  // enough groups to put >= 8 waves per CU on a 256-CU part, each group >= 16 states
+  size_t groups = std::max<size_t>(1, std::min<size_t>(n / 16, (2048 * 64) / std::max(1u, gx * 4)));
+  groups = std::min<size_t>(groups, 65535);
+  if (groups <= 1) {
+    hipLaunchKernelGGL(k_and_rows, dim3(gx), dim3(256), 0, s, states, n, state_bytes, out, 0);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+  const size_t glen = (n + groups - 1) / groups;
+  groups = (n + glen - 1) / glen;
+  uint8_t *partial = nullptr;
+  HIP_TRY(hipMallocAsync((void **)&partial, groups * state_bytes, s));
+  hipLaunchKernelGGL(k_and_groups, dim3(gx, (unsigned)groups), dim3(256), 0, s, states, n,
+                     state_bytes, glen, partial);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_and_rows, dim3(gx), dim3(256), 0, s, partial, groups, state_bytes, out, 0);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipFreeAsync(partial, s));
+  return 0;
+}
+
+int kbz_merge_and_host(uint8_t *out, const uint8_t *states, size_t n, size_t state_bytes) {
+  if (!out || (!states && n)) return fail("null argument");
+  if (state_bytes == 0) return 0;
+  if (n == 0) {
+    memset(out, 0xff, state_bytes);
+    return 0;
+  }
+  const size_t per = std::max<size_t>(1, (256u << 20) / state_bytes);
+  hipStream_t cs, ws;
+  HIP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&ws, hipStreamNonBlocking));
+  uint8_t *pin[2] = {nullptr, nullptr}, *dst[2] = {nullptr, nullptr}, *acc = nullptr,
+          *part = nullptr;
+  hipEvent_t copied[2], used[2];
+  const size_t cap = std::min(per, n);
+  for (int i = 0; i < 2; i++) {
+    HIP_TRY(hipHostMalloc((void **)&pin[i], cap * state_bytes, hipHostMallocDefault));
+    HIP_TRY(hipMalloc((void **)&dst[i], cap * state_bytes));
+    HIP_TRY(hipEventCreateWithFlags(&copied[i], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&used[i], hipEventDisableTiming));
+  }
+  HIP_TRY(hipMalloc((void **)&acc, state_bytes));
+  HIP_TRY(hipMalloc((void **)&part, state_bytes));
+  HIP_TRY(hipMemsetAsync(acc, 0xff, state_bytes, ws));
+  int rc = 0;
+  for (size_t lo = 0, b = 0; lo < n; lo += cap, b++) {
+    const int sl = (int)(b & 1);
+    const size_t cnt = std::min(cap, n - lo);
+    HIP_TRY(hipEventSynchronize(used[sl]));
+    memcpy(pin[sl], states + lo * state_bytes, cnt * state_bytes);
+    HIP_TRY(hipMemcpyAsync(dst[sl], pin[sl], cnt * state_bytes, hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipEventRecord(copied[sl], cs));
+    HIP_TRY(hipStreamWaitEvent(ws, copied[sl], 0));
+    if ((rc = kbz_merge_and_device(part, dst[sl], cnt, state_bytes, ws))) break;
+    if (state_bytes % 16 == 0) {
+      hipLaunchKernelGGL(k_and_rows, dim3(cdiv(state_bytes / 16, 256)), dim3(256), 0, ws, part,
+                         (size_t)1, state_bytes, acc, 1);
+    } else {
+      hipLaunchKernelGGL(k_and_bytes, dim3(cdiv(state_bytes, 256)), dim3(256), 0, ws, part,
+                         (size_t)1, state_bytes, acc, 1);
+    }
+    HIP_TRY(hipEventRecord(used[sl], ws));
+  }
+  if (!rc) {
+    HIP_TRY(hipStreamSynchronize(ws));
+    HIP_TRY(hipMemcpy(out, acc, state_bytes, hipMemcpyDeviceToHost));
+  }
+  for (int i = 0; i < 2; i++) {
+    (void)hipHostFree(pin[i]);
+    (void)hipFree(dst[i]);
+    (void)hipEventDestroy(copied[i]);
+    (void)hipEventDestroy(used[i]);
+  }
+  (void)hipFree(acc);
+  (void)hipFree(part);
+  (void)hipStreamDestroy(cs);
+  (void)hipStreamDestroy(ws);
+  return rc;
+}
+
+// ---- standalone hashes ---------------------------------------------------------------------------
+int kbz_hash32_device(const uint8_t *rows, size_t n, size_t stride, size_t len, uint32_t seed,
+                      uint32_t *h32_out, void *stream) {
+  if (len % 8) return fail("hash32 needs len % 8 == 0 (afl_progs/hash.h:38)");
+  if (!n) return 0;
+  if (!rows || !h32_out) return fail("null argument");
+  hipLaunchKernelGGL(k_rowhash32, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, rows, n,
+                     stride, len, seed, h32_out);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+int kbz_xxh64_device(const uint8_t *rows, size_t n, size_t stride, size_t len, uint64_t seed,
+                     uint64_t *x64_out, void *stream) {
+  if (!n) return 0;
+  if (!rows || !x64_out) return fail("null argument");
+  hipLaunchKernelGGL(k_rowxxh64, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, rows, n,
+                     stride, len, seed, x64_out);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,76 @@
+"""Multi-GPU sharded triage: one process per GPU, torch.distributed (RCCL over xGMI).
+
+A batch of N traces is split into contiguous shards, rank g holding [lo_g, hi_g).  Order is
+preserved, so the reference's sequential semantics hold across shards once every rank knows
+the OR of the coverage seen by the ranks before it:
+
+  1. local pass over the shard (kbz_shard_begin: hashes, chunk aggregates)   -- no traffic
+  2. DynamoRIO only: all-gather of each shard's last hash32 (8 B per rank); the first trace
+     of a shard is compared with the last trace of the nearest non-empty earlier shard
+  3. local OR aggregate per virgin map (kbz_shard_reduce)
+  4. all-gather of the aggregates (nclass * map_size bytes per rank) -> prefix = OR of earlier
+     ranks, total = OR of all ranks.  RCCL has no bitwise reductions, so this is an
+     all-gather plus a local OR (kbz_or_reduce), ~8 x 64 KiB over xGMI: latency-bound.
+  5. local resolve with the prefix; every rank applies V' = V & ~total, so the virgin maps
+     stay identical on all ranks.
+
+The engine is any object with the shard_* methods of killerbeez_amd.triage.TriageContext
+(tests plug a CPU engine in to exercise this protocol with the gloo backend).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+MODE_DYNAMORIO = 1
+
+
+def split_counts(n_total: int, world: int) -> list[int]:
+    return [n_total * (r + 1) // world - n_total * r // world for r in range(world)]
+
+
+def _all_gather(t: torch.Tensor, world: int, group=None) -> torch.Tensor:
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t, group=group)
+    return torch.stack(parts)
+
+
+def triage_sharded(engine, traces, outcome, counts, rank, world, want=1, group=None,
+                   device=None, timings=None):
+    """Run one rank's part of a sharded batch.  counts[r] = number of traces on rank r (host
+    ints, known to every rank).  Returns the engine's output dict (hnb, h32, ...)."""
+    device = device if device is not None else traces.device
+    ev = None
+    if timings is not None:
+        ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+        ev[0].record()
+    out = engine.shard_begin(traces, outcome, want)
+    if ev is not None:
+        ev[1].record()
+        timings.append(ev)
+    nonempty = [r for r in range(world) if counts[r] > 0]
+    if engine.mode == MODE_DYNAMORIO:
+        pair = torch.empty(2, dtype=torch.int32, device=device)
+        engine.shard_last_hash(pair)
+        pairs = _all_gather(pair, world, group) if world > 1 else pair.view(1, 2)
+        prev = [r for r in nonempty if r < rank]
+        prev_t = pairs[prev[-1]] if prev else None
+        glob_t = pairs[nonempty[-1]] if nonempty else None
+        engine.shard_link(prev_t, not prev, glob_t)
+    else:
+        engine.shard_link(None, True, None)
+    engine.shard_reduce()
+    nb = engine.shard_aggregate_bytes()
+    agg = torch.empty(nb, dtype=torch.uint8, device=device)
+    engine.shard_aggregate(agg)
+    if world > 1:
+        allagg = _all_gather(agg, world, group)
+        total = torch.empty(nb, dtype=torch.uint8, device=device)
+        engine.or_reduce(total, allagg, 0, world, nb)
+        prefix = None
+        if rank > 0:
+            prefix = torch.empty(nb, dtype=torch.uint8, device=device)
+            engine.or_reduce(prefix, allagg, 0, rank, nb)
+    else:
+        total, prefix = agg, None
+    return engine.shard_finish(prefix, total)

@@ -1,0 +1,270 @@
+"""Host-side handle on the gfx950 triage engine (over include/kbz_triage.h via ctypes).
+
+Device memory and streams come from PyTorch (``torch.cuda`` tensors and their
+``data_ptr()``; ``torch.cuda.current_stream().cuda_stream``); all arithmetic runs in the HIP
+kernels of libkbz_hip.so.  See include/kbz_triage.h for the reference functions each call
+replaces.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import KbzError, check, lib
+
+MODE_AFL, MODE_DYNAMORIO, MODE_AFL_CLASSIFY = 0, 1, 2
+FUZZ_NONE, FUZZ_HANG, FUZZ_CRASH = 0, 1, 2
+WANT_H32, WANT_X64 = 1, 2
+MODES = {"afl": MODE_AFL, "dynamorio": MODE_DYNAMORIO, "afl_classify": MODE_AFL_CLASSIFY}
+
+
+def _np_ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _stream_handle(stream):
+    import torch
+
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return C.c_void_p(stream.cuda_stream)
+
+
+def nclass(mode: int) -> int:
+    return 1 if mode == MODE_DYNAMORIO else 3
+
+
+class TriageContext:
+    """One virgin-map state (3 maps) + workspace on the current GPU.
+
+    Mirrors the bitmap half of the AFL/DynamoRIO instrumentation state
+    (instrumentation/afl_instrumentation.h:12-34): virgin_bits/tmout/crash, last hash."""
+
+    def __init__(self, map_size: int = 65536, mode: int | str = MODE_AFL,
+                 max_batch: int = 65536):
+        if isinstance(mode, str):
+            mode = MODES[mode]
+        self.map_size, self.mode, self.max_batch = int(map_size), int(mode), int(max_batch)
+        L = lib()
+        self._h = L.kbz_ctx_create(self.map_size, self.mode, self.max_batch)
+        if not self._h:
+            raise KbzError("kbz_ctx_create: " + (L.kbz_last_error() or b"").decode())
+
+    # -- lifetime --------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().kbz_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    # -- state -----------------------------------------------------------------------------
+    def get_virgin(self) -> np.ndarray:
+        out = np.empty((3, self.map_size), np.uint8)
+        check(lib().kbz_get_virgin(self._h, _np_ptr(out)), "kbz_get_virgin")
+        return out
+
+    def set_virgin(self, v: np.ndarray) -> None:
+        v = np.ascontiguousarray(v, dtype=np.uint8).reshape(3, self.map_size)
+        check(lib().kbz_set_virgin(self._h, _np_ptr(v)), "kbz_set_virgin")
+
+    @property
+    def last_hash(self) -> int:
+        x = C.c_uint32()
+        check(lib().kbz_get_last_hash(self._h, C.byref(x)), "kbz_get_last_hash")
+        return x.value
+
+    @last_hash.setter
+    def last_hash(self, v: int) -> None:
+        check(lib().kbz_set_last_hash(self._h, int(v) & 0xFFFFFFFF), "kbz_set_last_hash")
+
+    def set_ignore(self, ignore) -> None:
+        if ignore is None:
+            check(lib().kbz_set_ignore(self._h, None), "kbz_set_ignore")
+            return
+        ig = np.ascontiguousarray(ignore, dtype=np.uint8).reshape(self.map_size)
+        check(lib().kbz_set_ignore(self._h, _np_ptr(ig)), "kbz_set_ignore")
+
+    def sync(self, stream=None) -> None:
+        check(lib().kbz_sync(self._h, _stream_handle(stream)), "kbz_sync")
+
+    # -- triage ----------------------------------------------------------------------------
+    def triage(self, traces, outcome=None, want: int = WANT_H32, out=None, stream=None):
+        """Device-resident batch: traces is a CUDA uint8 tensor [n, map_size] (rows may be
+        strided).  Returns dict of CUDA tensors hnb (uint8), h32 (int32 view of uint32),
+        x64 (int64 view of uint64; only with WANT_X64)."""
+        import torch
+
+        assert traces.is_cuda and traces.dtype == torch.uint8 and traces.dim() == 2
+        n = traces.shape[0]
+        if n and traces.shape[1] != self.map_size:
+            raise ValueError("trace rows must be map_size bytes")
+        stride = traces.stride(0) if n else self.map_size
+        if n and traces.stride(1) != 1:
+            raise ValueError("trace rows must be contiguous")
+        dev = traces.device
+        if out is None:
+            out = {"hnb": torch.empty(n, dtype=torch.uint8, device=dev)}
+            if want & WANT_H32:
+                out["h32"] = torch.empty(n, dtype=torch.int32, device=dev)
+            if want & WANT_X64:
+                out["x64"] = torch.empty(n, dtype=torch.int64, device=dev)
+        oc = None
+        if outcome is not None:
+            oc = outcome.to(device=dev, dtype=torch.int8).contiguous()
+        rc = lib().kbz_triage_batch_device(
+            self._h, C.c_void_p(traces.data_ptr()), n, stride,
+            None if oc is None else C.c_void_p(oc.data_ptr()),
+            C.c_void_p(out["hnb"].data_ptr()),
+            C.c_void_p(out["h32"].data_ptr()) if "h32" in out else None,
+            C.c_void_p(out["x64"].data_ptr()) if "x64" in out else None,
+            want, _stream_handle(stream))
+        check(rc, "kbz_triage_batch_device")
+        return out
+
+    def triage_host(self, traces: np.ndarray, outcome=None, want: int = WANT_H32):
+        """Host-memory batch (numpy uint8 [n, map_size]); streamed through pinned slots."""
+        t = np.ascontiguousarray(traces, dtype=np.uint8)
+        n = t.shape[0]
+        oc = None if outcome is None else np.ascontiguousarray(outcome, dtype=np.int8)
+        hnb = np.zeros(n, np.uint8)
+        h32 = np.zeros(n, np.uint32) if want & WANT_H32 else None
+        x64 = np.zeros(n, np.uint64) if want & WANT_X64 else None
+        rc = lib().kbz_triage_batch_host(self._h, _np_ptr(t), n, self.map_size, _np_ptr(oc),
+                                         _np_ptr(hnb), _np_ptr(h32), _np_ptr(x64), want)
+        check(rc, "kbz_triage_batch_host")
+        res = {"hnb": hnb}
+        if h32 is not None:
+            res["h32"] = h32
+        if x64 is not None:
+            res["x64"] = x64
+        return res
+
+    # -- sharded triage (one rank's part; see killerbeez_amd.dist) --------------------------
+    def shard_begin(self, traces, outcome=None, want=WANT_H32, out=None, stream=None):
+        import torch
+
+        n = traces.shape[0]
+        stride = traces.stride(0) if n else self.map_size
+        dev = traces.device
+        if out is None:
+            out = {"hnb": torch.empty(n, dtype=torch.uint8, device=dev)}
+            if want & WANT_H32:
+                out["h32"] = torch.empty(n, dtype=torch.int32, device=dev)
+            if want & WANT_X64:
+                out["x64"] = torch.empty(n, dtype=torch.int64, device=dev)
+        self._oc = None if outcome is None else outcome.to(device=dev, dtype=torch.int8).contiguous()
+        self._out = out
+        rc = lib().kbz_shard_begin(
+            self._h, C.c_void_p(traces.data_ptr()) if n else None, n, stride,
+            None if self._oc is None else C.c_void_p(self._oc.data_ptr()),
+            C.c_void_p(out["h32"].data_ptr()) if "h32" in out else None,
+            C.c_void_p(out["x64"].data_ptr()) if "x64" in out else None,
+            want, _stream_handle(stream))
+        check(rc, "kbz_shard_begin")
+        return out
+
+    def shard_last_hash(self, out, stream=None):
+        """Copy {h32 of this shard's last trace, nonempty} into CUDA int32 tensor out[2]."""
+        check(lib().kbz_shard_last_hash(self._h, C.c_void_p(out.data_ptr()),
+                                        _stream_handle(stream)), "kbz_shard_last_hash")
+        return out
+
+    def shard_link(self, prev_last, is_first, global_last, stream=None):
+        """prev_last / global_last: CUDA int32 tensors [2] (or None)."""
+        ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        check(lib().kbz_shard_link(self._h, ptr(prev_last), int(bool(is_first)), ptr(global_last),
+                                   _stream_handle(stream)), "kbz_shard_link")
+
+    def shard_reduce(self, stream=None):
+        check(lib().kbz_shard_reduce(self._h, _stream_handle(stream)), "kbz_shard_reduce")
+
+    def shard_aggregate(self, out, stream=None):
+        """Copy this shard's OR aggregate into CUDA uint8 tensor out[nclass*map_size]."""
+        check(lib().kbz_shard_aggregate(self._h, C.c_void_p(out.data_ptr()),
+                                        _stream_handle(stream)), "kbz_shard_aggregate")
+        return out
+
+    def shard_aggregate_bytes(self) -> int:
+        return lib().kbz_shard_aggregate_bytes(self._h)
+
+    def shard_finish(self, prefix, total, stream=None):
+        out = self._out
+        check(lib().kbz_shard_finish(self._h, None if prefix is None else C.c_void_p(prefix.data_ptr()),
+                                     C.c_void_p(total.data_ptr()), C.c_void_p(out["hnb"].data_ptr()),
+                                     _stream_handle(stream)), "kbz_shard_finish")
+        return out
+
+    @staticmethod
+    def or_reduce(out, stacked, r_lo, r_hi, nbytes, stream=None):
+        return or_reduce(out, stacked, r_lo, r_hi, nbytes, stream)
+
+
+# ---- stateless device helpers ------------------------------------------------------------------
+
+def merge_and(states, out=None, stream=None):
+    """AND-fold of CUDA uint8 states [n, state_bytes] (merger/merger.c:79-99)."""
+    import torch
+
+    n = states.shape[0]
+    nbytes = states[0].numel() if n else 0
+    if out is None:
+        out = torch.empty(nbytes, dtype=torch.uint8, device=states.device)
+    check(lib().kbz_merge_and_device(C.c_void_p(out.data_ptr()),
+                                     C.c_void_p(states.data_ptr()) if n else None, n, nbytes,
+                                     _stream_handle(stream)), "kbz_merge_and_device")
+    return out
+
+
+def merge_and_host(states: np.ndarray) -> np.ndarray:
+    s = np.ascontiguousarray(states, dtype=np.uint8)
+    n = s.shape[0]
+    nbytes = s[0].size if n else 0
+    out = np.empty(nbytes, np.uint8)
+    check(lib().kbz_merge_and_host(_np_ptr(out), _np_ptr(s), n, nbytes), "kbz_merge_and_host")
+    return out
+
+
+def or_reduce(out, stacked, r_lo, r_hi, nbytes, stream=None):
+    check(lib().kbz_or_reduce(C.c_void_p(out.data_ptr()), C.c_void_p(stacked.data_ptr()), r_lo,
+                              r_hi, nbytes, _stream_handle(stream)), "kbz_or_reduce")
+    return out
+
+
+def hash32_rows(rows, length=None, seed=0xA5B35705, stream=None):
+    import torch
+
+    n = rows.shape[0]
+    length = rows.shape[1] if length is None else length
+    out = torch.empty(n, dtype=torch.int32, device=rows.device)
+    check(lib().kbz_hash32_device(C.c_void_p(rows.data_ptr()), n, rows.stride(0), length, seed,
+                                  C.c_void_p(out.data_ptr()), _stream_handle(stream)),
+          "kbz_hash32_device")
+    return out
+
+
+def xxh64_rows(rows, length=None, seed=0, stream=None):
+    import torch
+
+    n = rows.shape[0]
+    length = rows.shape[1] if length is None else length
+    out = torch.empty(n, dtype=torch.int64, device=rows.device)
+    check(lib().kbz_xxh64_device(C.c_void_p(rows.data_ptr()), n, rows.stride(0), length, seed,
+                                 C.c_void_p(out.data_ptr()), _stream_handle(stream)),
+          "kbz_xxh64_device")
+    return out

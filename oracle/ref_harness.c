@@ -1,0 +1,102 @@
+/*
+ * oracle/ref_harness.c -- TEST INFRASTRUCTURE ONLY (never shipped, never measured as the product).
+ *
+ * Exposes the reference's OWN bitmap code, compiled from the files under /root/reference,
+ * through plain C entry points so the clean-room restatement (oracle/kbz_oracle.c) and the
+ * committed golden fixtures can be pinned against it.  Built by oracle/Makefile into
+ * oracle/_ref/libkbz_ref.so; nothing of the reference is copied into the repository: the
+ * function bodies are pulled in at build time with #include / sed-extracted .inc files that
+ * live only in oracle/_ref/ (git-ignored).
+ *
+ * One translation unit per (source, MAP_SIZE) pair, selected with -D flags by the Makefile:
+ *   REF_AFL   instrumentation/afl_instrumentation.c:116-121 (merge_bitmaps),
+ *             :600-707 (has_new_bits, simplify_lookup, simplify_trace)   [x86_64 variants]
+ *   REF_DR    instrumentation/dynamorio_instrumentation.c:79-339 (has_new_bits,
+ *             has_new_bits_with_ignore, count_class_lookup, classify_counts, merge_bitmaps)
+ *   REF_HASH  afl_progs/hash.h:36-65 (hash32) and instrumentation/winafl_hash.h:80-112
+ *             (hash32_with_ignore), instrumentation/xxhash.h + xxhash.c:855 (XXH64, v0.6.5)
+ * MAP_SIZE is a compile-time constant in the reference (afl_progs/config.h:314-315); the
+ * Makefile builds the 64 KiB and 1 MiB variants by defining it before the extracted code.
+ */
+#include <stdint.h>
+#include <stddef.h>
+#include <string.h>
+
+#ifndef REF_SUFFIX
+#error "REF_SUFFIX must be defined (e.g. 64k)"
+#endif
+#define REF_CAT2(a, b) a##_##b
+#define REF_CAT(a, b) REF_CAT2(a, b)
+#define REF_NAME(n) REF_CAT(n, REF_SUFFIX)
+
+#if defined(REF_AFL)
+#include "types.h" /* /root/reference/afl_progs/types.h: u8.., likely/unlikely */
+#define merge_bitmaps REF_NAME(afl_merge_bitmaps_impl) /* non-static in the reference: keep TUs apart */
+#include "afl_merge.inc"
+#include "afl_bitmap.inc"
+uint8_t REF_NAME(ref_afl_has_new_bits)(uint8_t *virgin, uint8_t *trace) {
+  return has_new_bits(virgin, trace);
+}
+void REF_NAME(ref_afl_simplify_trace)(uint8_t *trace) { simplify_trace((uint64_t *)trace); }
+void REF_NAME(ref_afl_merge_bitmaps)(uint8_t *dest, const uint8_t *src) { merge_bitmaps(dest, src); }
+size_t REF_NAME(ref_afl_map_size)(void) { return MAP_SIZE; }
+
+#elif defined(REF_DR)
+#include "winafl_types.h" /* /root/reference/instrumentation/winafl_types.h */
+#define merge_bitmaps REF_NAME(dr_merge_bitmaps_impl)
+#include "dr_bitmap.inc"
+uint8_t REF_NAME(ref_dr_has_new_bits)(uint8_t *trace, uint8_t *virgin) {
+  return has_new_bits(trace, virgin);
+}
+uint8_t REF_NAME(ref_dr_has_new_bits_with_ignore)(uint8_t *trace, uint8_t *virgin, uint8_t *ignore) {
+  return has_new_bits_with_ignore(trace, virgin, ignore);
+}
+void REF_NAME(ref_dr_classify_counts)(uint8_t *trace) { classify_counts((u64 *)trace); }
+void REF_NAME(ref_dr_merge_bitmaps)(uint8_t *dest, const uint8_t *src) { merge_bitmaps(dest, src); }
+uint8_t REF_NAME(ref_dr_count_class)(uint8_t c) { return count_class_lookup[c]; }
+
+#include "winafl_hash.h" /* /root/reference/instrumentation/winafl_hash.h: hash32 (x86_64) */
+/* The per-exec DynamoRIO novelty step as the reference runs it, exec after exec: the control
+ * flow of has_new_coverage (dynamorio_instrumentation.c:1428-1468, without the Windows-only
+ * debug dump) over the reference's own classify_counts / hash32 / has_new_bits.  This is the
+ * CPU baseline bench.py times ("kind": "reference").  scratch: MAP_SIZE bytes (the SHM copy). */
+void REF_NAME(ref_dr_triage_loop)(const uint8_t *traces, size_t n, size_t stride, uint8_t *virgin,
+                                  uint32_t *last_hash, uint8_t *hnb_out, uint8_t *scratch) {
+  uint32_t last = *last_hash;
+  for (size_t j = 0; j < n; j++) {
+    memcpy(scratch, traces + j * stride, MAP_SIZE);
+    classify_counts((u64 *)scratch);
+    uint32_t h = hash32(scratch, MAP_SIZE, 0xa5b35705u /* HASH_CONST winafl_config.h:330 */);
+    if (h == last) {
+      hnb_out[j] = 0;
+      continue;
+    }
+    last = h;
+    hnb_out[j] = has_new_bits(scratch, virgin);
+  }
+  *last_hash = last;
+}
+
+#elif defined(REF_HASH)
+#include "hash.h" /* /root/reference/afl_progs/hash.h (x86_64 hash32) */
+uint32_t REF_NAME(ref_hash32)(const void *key, uint32_t len, uint32_t seed) {
+  return hash32(key, len, seed);
+}
+#elif defined(REF_HASH_IGNORE)
+#include "winafl_hash.h" /* /root/reference/instrumentation/winafl_hash.h */
+uint32_t REF_NAME(ref_winafl_hash32)(const void *key, uint32_t len, uint32_t seed) {
+  return hash32(key, len, seed);
+}
+uint32_t REF_NAME(ref_hash32_with_ignore)(const void *key, const void *ignore, uint32_t len,
+                                          uint32_t seed) {
+  return hash32_with_ignore(key, ignore, len, seed);
+}
+#elif defined(REF_XXH)
+#include "xxhash.h" /* /root/reference/instrumentation/xxhash.h: XXH_INLINE_ALL pulls xxhash.c */
+unsigned long long REF_NAME(ref_xxh64)(const void *input, size_t len, unsigned long long seed) {
+  return XXH64(input, len, seed);
+}
+unsigned REF_NAME(ref_xxh_version)(void) { return XXH_versionNumber(); }
+#else
+#error "select one of REF_AFL / REF_DR / REF_HASH / REF_HASH_IGNORE / REF_XXH"
+#endif

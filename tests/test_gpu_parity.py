@@ -1,0 +1,250 @@
+"""Bit-exact parity of the gfx950 path (libkbz_hip.so through the C ABI) with the CPU oracle.
+
+The oracle (oracle/kbz_oracle.c) is itself pinned to the reference's own code by
+tests/test_oracle_pin.py and to tests/golden/ by tests/test_golden.py.  Every comparison here
+is exact: per-trace has_new_bits results, hash32, XXH64, the three virgin maps and the
+DynamoRIO last hash.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from killerbeez_amd import synth
+from killerbeez_amd.triage import (MODE_AFL, MODE_AFL_CLASSIFY, MODE_DYNAMORIO, WANT_H32,
+                                   WANT_X64, TriageContext, hash32_rows, merge_and,
+                                   merge_and_host, xxh64_rows)
+
+pytestmark = pytest.mark.gpu
+MODES = [MODE_AFL, MODE_DYNAMORIO, MODE_AFL_CLASSIFY]
+
+
+def gpu_triage(ctx, traces, oc, want=WANT_H32 | WANT_X64):
+    import torch
+
+    t = torch.from_numpy(np.ascontiguousarray(traces)).cuda()
+    o = None if oc is None else torch.from_numpy(np.ascontiguousarray(oc)).cuda()
+    out = ctx.triage(t, o, want)
+    torch.cuda.synchronize()
+    ctx.sync()
+    res = {"hnb": out["hnb"].cpu().numpy()}
+    if "h32" in out:
+        res["h32"] = out["h32"].cpu().numpy().view(np.uint32)
+    if "x64" in out:
+        res["x64"] = out["x64"].cpu().numpy().view(np.uint64)
+    return res
+
+
+def check(mode, traces, oc, ignore=None, virgin=None, last=0, want=WANT_H32 | WANT_X64,
+          ctx=None, max_batch=None):
+    n, m = traces.shape
+    own = ctx is None
+    if own:
+        ctx = TriageContext(m, mode, max_batch or max(n, 1))
+        if ignore is not None:
+            ctx.set_ignore(ignore)
+        if virgin is not None:
+            ctx.set_virgin(virgin)
+        ctx.last_hash = last
+    v0 = ctx.get_virgin()
+    l0 = ctx.last_hash
+    exp = oracle.triage_batch(mode, traces, oc, virgin=v0, ignore=ignore, last_hash=l0,
+                              want=oracle.WANT_H32 | oracle.WANT_X64)
+    got = gpu_triage(ctx, traces, oc, want)
+    np.testing.assert_array_equal(got["hnb"], exp["hnb"])
+    if want & WANT_H32:
+        np.testing.assert_array_equal(got["h32"], exp["h32"])
+    if want & WANT_X64:
+        np.testing.assert_array_equal(got["x64"], exp["x64"])
+    np.testing.assert_array_equal(ctx.get_virgin(), exp["virgin"])
+    if mode == MODE_DYNAMORIO:
+        assert ctx.last_hash == exp["last_hash"]
+    if own:
+        ctx.close()
+    return exp
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_sparse_64k_partial_chunk(gpu, mode):
+    t, oc = synth.sparse_np(1000, 65536, seed=100 + mode)
+    exp = check(mode, t, oc)
+    assert exp["hnb"].max() == 2
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("density", [0.02, 0.3, 1.0])
+def test_uniform_density(gpu, mode, density):
+    t = synth.uniform_np(200, 65536, seed=int(density * 100), density=density)
+    rng = np.random.default_rng(7)
+    oc = rng.choice(3, size=200, p=[0.7, 0.15, 0.15]).astype(np.int8)
+    check(mode, t, oc)
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("m", [256, 4096, 1 << 20])
+def test_map_sizes(gpu, mode, m):
+    t, oc = synth.sparse_np(130, m, seed=m + mode, hot_frac=0.05)
+    check(mode, t, oc)
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65])
+def test_small_batches(gpu, mode, n):
+    t, oc = synth.sparse_np(n, 4096, seed=n)
+    check(mode, t, oc)
+
+
+def test_dynamorio_identical_runs_and_chunk_boundary(gpu):
+    t, oc = synth.sparse_np(300, 65536, seed=3)
+    t[10:20] = t[9]        # a run inside a chunk
+    t[64] = t[63]          # across the chunk boundary
+    t[128:140] = t[127]    # run that starts a chunk
+    t[200] = t[198]        # equal to a non-neighbour: not skipped
+    exp = check(MODE_DYNAMORIO, t, oc)
+    assert (exp["hnb"][10:20] == 0).all() and exp["hnb"][64] == 0
+
+
+def test_dynamorio_last_hash_carried_across_batches(gpu):
+    t, oc = synth.sparse_np(200, 65536, seed=4)
+    ctx = TriageContext(65536, MODE_DYNAMORIO, 200)
+    check(MODE_DYNAMORIO, t[:100], oc[:100], ctx=ctx)
+    t2 = t[100:].copy()
+    t2[0] = t[99]  # first trace of batch 2 equals the last of batch 1 -> skipped
+    t2[64] = t2[63]
+    exp = check(MODE_DYNAMORIO, t2, oc[100:], ctx=ctx)
+    assert exp["hnb"][0] == 0
+    ctx.close()
+
+
+def test_dynamorio_ignore_skips_that_differ(gpu):
+    """hash32_with_ignore masks bytes whose ignore byte is 0, has_new_bits_with_ignore only
+    looks at those bytes: equal hashes with different examined bytes must be excluded from
+    the virgin update (the chunk-recompute path)."""
+    rng = np.random.default_rng(5)
+    m = 65536
+    t, oc = synth.sparse_np(400, m, seed=6)
+    ign = np.where(rng.random(m) < 0.4, 0, rng.integers(1, 256, size=m)).astype(np.uint8)
+    zc = np.nonzero(ign == 0)[0]
+    for j in (5, 64, 65, 130, 131, 132, 399):
+        t[j] = t[j - 1]
+        t[j, rng.choice(zc, 20)] = rng.integers(1, 256, 20)
+    check(MODE_DYNAMORIO, t, oc, ignore=ign)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_preset_virgin_and_sequential_composition(gpu, mode):
+    m = 65536
+    rng = np.random.default_rng(8)
+    v = rng.integers(0, 256, size=(3, m)).astype(np.uint8)
+    v[:, rng.random(m) < 0.5] = 0xFF
+    t, oc = synth.sparse_np(700, m, seed=9)
+    ctx = TriageContext(m, mode, 700)
+    ctx.set_virgin(v)
+    # three uneven batches in a row == one sequential pass
+    for lo, hi in ((0, 1), (1, 333), (333, 700)):
+        check(mode, t[lo:hi], oc[lo:hi], ctx=ctx)
+    whole = oracle.triage_batch(mode, t, oc, virgin=v)
+    np.testing.assert_array_equal(ctx.get_virgin(), whole["virgin"])
+    ctx.close()
+
+
+@pytest.mark.parametrize("mode", [MODE_AFL, MODE_AFL_CLASSIFY])
+def test_crash_hang_heavy(gpu, mode):
+    t, oc = synth.sparse_np(500, 65536, seed=12, outcome_p=(0.4, 0.3, 0.3))
+    check(mode, t, oc)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_strided_rows_and_no_outcome(gpu, mode):
+    import torch
+
+    m = 4096
+    t, oc = synth.sparse_np(150, m, seed=13)
+    big = np.zeros((150, m + 512), np.uint8)
+    big[:, :m] = t
+    ctx = TriageContext(m, mode, 150)
+    exp = oracle.triage_batch(mode, t, None, want=oracle.WANT_H32 | oracle.WANT_X64)
+    tt = torch.from_numpy(big).cuda()[:, :m]
+    out = ctx.triage(tt, None, WANT_H32 | WANT_X64)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["hnb"].cpu().numpy(), exp["hnb"])
+    np.testing.assert_array_equal(out["h32"].cpu().numpy().view(np.uint32), exp["h32"])
+    np.testing.assert_array_equal(out["x64"].cpu().numpy().view(np.uint64), exp["x64"])
+    np.testing.assert_array_equal(ctx.get_virgin(), exp["virgin"])
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_host_streaming_path(gpu, mode):
+    m = 65536
+    t, oc = synth.sparse_np(2500, m, seed=14)
+    ctx = TriageContext(m, mode, 2500)
+    exp = oracle.triage_batch(mode, t, oc, want=oracle.WANT_H32 | oracle.WANT_X64)
+    got = ctx.triage_host(t, oc, WANT_H32 | WANT_X64)
+    np.testing.assert_array_equal(got["hnb"], exp["hnb"])
+    np.testing.assert_array_equal(got["h32"], exp["h32"])
+    np.testing.assert_array_equal(got["x64"], exp["x64"])
+    np.testing.assert_array_equal(ctx.get_virgin(), exp["virgin"])
+
+
+@pytest.mark.parametrize("n,nbytes", [(0, 3 * 4096), (1, 3 * 4096), (37, 3 * 65536),
+                                      (1000, 3 * 65536), (20, 1000)])
+def test_merge(gpu, n, nbytes):
+    import torch
+
+    rng = np.random.default_rng(n)
+    s = rng.integers(0, 256, size=(n, nbytes)).astype(np.uint8) | rng.integers(
+        0, 256, size=(n, nbytes)).astype(np.uint8)
+    exp = oracle.merge_many(s) if n else np.full(nbytes, 0xFF, np.uint8)
+    got = merge_and(torch.from_numpy(s).cuda().reshape(n, nbytes)) if n else None
+    if got is not None:
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(got.cpu().numpy(), exp.reshape(-1))
+    np.testing.assert_array_equal(merge_and_host(s.reshape(n, nbytes)), exp.reshape(-1))
+
+
+def test_merge_states_property(gpu):
+    import torch
+
+    s = synth.merger_states_np(257, 4096, seed=1)
+    got = merge_and(torch.from_numpy(s).cuda()).cpu().numpy()
+    np.testing.assert_array_equal(got, np.bitwise_and.reduce(s, axis=0))
+
+
+@pytest.mark.parametrize("length", [8, 64, 256, 4096, 65536])
+def test_row_hashes(gpu, length):
+    import torch
+
+    rng = np.random.default_rng(length)
+    rows = rng.integers(0, 256, size=(70, length)).astype(np.uint8)
+    h = hash32_rows(torch.from_numpy(rows).cuda()).cpu().numpy().view(np.uint32)
+    x = xxh64_rows(torch.from_numpy(rows).cuda()).cpu().numpy().view(np.uint64)
+    for j in range(70):
+        assert h[j] == oracle.hash32(rows[j])
+        assert x[j] == oracle.xxh64(rows[j])
+    for ln in (1, 5, 31, 33, 100):
+        x = xxh64_rows(torch.from_numpy(rows).cuda(), length=min(ln, length), seed=3).cpu().numpy().view(np.uint64)
+        assert x[0] == oracle.xxh64(rows[0, :min(ln, length)], 3)
+
+
+@pytest.mark.slow
+def test_full_size_config2(gpu):
+    """BASELINE config 2 at full size: 65,536 sparse traces x 64 KiB, DynamoRIO mode, checked
+    exactly against the sharded CPU oracle, plus size-independent invariants."""
+    import torch
+
+    n, m = 65536, 65536
+    t, oc = synth.sparse_torch(n, m, seed=0x5EED, device="cuda")
+    ctx = TriageContext(m, MODE_DYNAMORIO, n)
+    out = ctx.triage(t, oc, WANT_H32)
+    torch.cuda.synchronize()
+    ctx.sync()
+    th = t.cpu().numpy()
+    exp = oracle.triage_batch(MODE_DYNAMORIO, th, oc.cpu().numpy(), threads=16)
+    np.testing.assert_array_equal(out["hnb"].cpu().numpy(), exp["hnb"])
+    np.testing.assert_array_equal(out["h32"].cpu().numpy().view(np.uint32), exp["h32"])
+    v = ctx.get_virgin()
+    np.testing.assert_array_equal(v, exp["virgin"])
+    # idempotence: the same batch again finds nothing new and leaves the virgin map alone
+    out2 = ctx.triage(t, oc, WANT_H32)
+    torch.cuda.synchronize()
+    assert int(out2["hnb"].max()) == 0
+    np.testing.assert_array_equal(ctx.get_virgin(), v)
