@@ -95,7 +95,7 @@ def cpu_baseline_all_cores(traces_dev, mode, seconds):
 
     import oracle
 
-    threads = min(os.cpu_count() or 1, 64)
+    threads = min(os.cpu_count() or 1, 16)  # the GPU box's CPU share is 16 threads
     sample_n = min(traces_dev.shape[0], 8192)
     host = traces_dev[:sample_n].cpu().numpy()
     done, t0 = 0, time.perf_counter()
