@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -83,6 +84,12 @@ __device__ __forceinline__ uint64_t from_prev_lane(uint64_t v) {
   const uint32_t lo = __shfl_up((uint32_t)v, 1), hi = __shfl_up((uint32_t)(v >> 32), 1);
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// streaming 16-B load of data read exactly once (nontemporal: do not keep it in L2)
+__device__ __forceinline__ uint4 ld_stream16(const uint8_t *p) {
+  const u32x4 v = __builtin_nontemporal_load((const u32x4 *)p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ uint64_t ld_u64(const uint4 &v, int e) {
   return e ? ((uint64_t)v.z | ((uint64_t)v.w << 32)) : ((uint64_t)v.x | ((uint64_t)v.y << 32));
 }
@@ -115,14 +122,19 @@ struct Pass1Args {
 
 // ---------------------------------------------------------------------------------------------
 // pass 1: one wave per chunk of 64 consecutive traces, lane = trace.
-// LDS tile = 64 rows x 256 B; 16-B slot q of row r lives at slot q ^ (r & 15) so both the
-// coalesced fill (4 rows per wave-instruction) and the row-per-lane ds_read_b128 are
-// conflict-free.
+// Each tile stages TW bytes of all 64 rows in LDS (TW = 512: 32 KiB, loaded as 32 coalesced
+// 1-KiB wave-instructions and kept in flight in registers while the previous tile is processed).
+// 16-B slot q of row r lives at slot q ^ (r & 15): the fill (2 rows per wave-instruction,
+// ds_write_b128) and the row-per-lane ds_read_b128 are both bank-conflict-free.
 // ---------------------------------------------------------------------------------------------
-template <int MODE, bool IGN, bool X64>
+template <int MODE, bool IGN, bool X64, int TW>
 __global__ __launch_bounds__(64) void k_pass1(Pass1Args a) {
   constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
-  __shared__ uint4 lds[kChunk * kTileW / 16];
+  constexpr int SLOTS = TW / 16;          // 16-B slots per row
+  constexpr int RPI = 64 / SLOTS;         // rows per wave-instruction (1 KiB each)
+  constexpr int NLD = 64 / RPI;           // loads per lane per tile
+  constexpr int WORDS = TW / 8;
+  __shared__ uint4 lds[kChunk * SLOTS];
   const int lane = threadIdx.x;
   const uint32_t chunk = blockIdx.x;
   const uint64_t row0 = (uint64_t)chunk * kChunk;
@@ -142,18 +154,25 @@ __global__ __launch_bounds__(64) void k_pass1(Pass1Args a) {
     a.chunk_cls[chunk] = m;
   }
 
-  const uint8_t *base = a.traces + row0 * a.stride;
-  const int lr = lane >> 4, ls = lane & 15;
-  const uint32_t ntiles = a.map_size / kTileW;
-  uint4 buf[16];
+  const int lr = lane / SLOTS, ls = lane % SLOTS;
+  const uint32_t ntiles = a.map_size / TW;
+  // row this lane loads in instruction i is RPI*i + lr; rows past the end of a partial
+  // chunk re-read the last valid row and are zeroed (no per-load branches)
+  const uint8_t *lbase = a.traces + row0 * a.stride + ls * 16;
+  uint4 buf[NLD];
   auto load_tile = [&](uint32_t t) {
+    const uint8_t *p = lbase + (size_t)t * TW;
+    if (nrows == kChunk) {
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int r = 4 * i + lr;
-      if (r < nrows)
-        buf[i] = *(const uint4 *)(base + (size_t)r * a.stride + (size_t)t * kTileW + ls * 16);
-      else
-        buf[i] = make_uint4(0, 0, 0, 0);
+      for (int i = 0; i < NLD; i++)
+        buf[i] = ld_stream16(p + (size_t)(RPI * i + lr) * a.stride);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NLD; i++) {
+        const int r = RPI * i + lr;
+        const uint4 v = *(const uint4 *)(p + (size_t)min(r, nrows - 1) * a.stride);
+        buf[i] = r < nrows ? v : make_uint4(0, 0, 0, 0);
+      }
     }
   };
 
@@ -165,62 +184,75 @@ __global__ __launch_bounds__(64) void k_pass1(Pass1Args a) {
   load_tile(0);
   for (uint32_t t = 0; t < ntiles; t++) {
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int r = 4 * i + lr;
-      lds[r * 16 + (ls ^ (r & 15))] = buf[i];
+    for (int i = 0; i < NLD; i++) {
+      const int r = RPI * i + lr;
+      lds[r * SLOTS + (ls ^ (r & 15))] = buf[i];
     }
     __syncthreads();
     if (t + 1 < ntiles) load_tile(t + 1);
 
-    const uint64_t *ig = IGN ? (const uint64_t *)(a.ignore + (size_t)t * kTileW) : nullptr;
+    const uint64_t *ig = IGN ? (const uint64_t *)(a.ignore + (size_t)t * TW) : nullptr;
     uint64_t orw[NC];
 #pragma unroll
     for (int k = 0; k < NC; k++) orw[k] = 0;
+    // 2 slots = 4 words per iteration: XXH64 lane (word & 3) stays a compile-time index
+#pragma unroll 1
+    for (int q = 0; q < SLOTS; q += 2) {
 #pragma unroll
-    for (int q = 0; q < 16; q++) {
-      const uint4 v = lds[lane * 16 + (q ^ (lane & 15))];
+      for (int qq = 0; qq < 2; qq++) {
+        const uint4 v = lds[lane * SLOTS + ((q + qq) ^ (lane & 15))];
 #pragma unroll
-      for (int e = 0; e < 2; e++) {
-        const int wi = 2 * q + e;
-        const uint64_t x = ld_u64(v, e);
-        uint64_t tw, kw;
-        if (__ballot(x != 0)) {
-          tw = xform8(x, xf);
-          const uint64_t ignw = IGN ? ig[wi] : ~0ull;
-          kw = h32_mix(tw & ignw);
+        for (int e = 0; e < 2; e++) {
+          const int wi = 2 * (q + qq) + e;  // word index inside the tile
+          const uint64_t x = ld_u64(v, e);
+          uint64_t tw;
+          if (__ballot(x != 0)) {
+            tw = xform8(x, xf);
+            const uint64_t ignw = IGN ? ig[wi] : ~0ull;
+            h = h32_step(h, h32_mix(tw & ignw));
 #pragma unroll
-          for (int k = 0; k < NC; k++) {
-            if (present[k]) {
-              const uint64_t r = wave_or64((valid && cls == k) ? tw : 0);
-              orw[k] = (lane == wi) ? r : orw[k];
+            for (int k = 0; k < NC; k++) {
+              if (present[k]) {
+                const uint64_t r = wave_or64((valid && cls == k) ? tw : 0);
+                orw[k] = (lane == (wi & 63)) ? r : orw[k];
+              }
             }
-          }
-          if (MODE == KBZ_MODE_DYNAMORIO) {
-            const uint64_t rel = IGN ? ~nonzero_bytes8(ignw) : ~0ull;
-            neq |= (tw ^ from_prev_lane(tw)) & rel;
-          }
-        } else {
-          tw = simp ? kSimpleZero : 0;
-          kw = simp ? ksimp : 0;
+            if (MODE == KBZ_MODE_DYNAMORIO) {
+              const uint64_t rel = IGN ? ~nonzero_bytes8(ignw) : ~0ull;
+              neq |= (tw ^ from_prev_lane(tw)) & rel;
+            }
+          } else if (MODE == KBZ_MODE_DYNAMORIO) {
+            tw = 0;
+            h = rotl64(h, 27) * 5 + 0x52dce729;  // h32_step(h, 0)
+          } else {
+            tw = simp ? kSimpleZero : 0;
+            h = h32_step(h, simp ? ksimp : 0);
 #pragma unroll
-          for (int k = 1; k < NC; k++)  // simplified classes see 0x01 bytes everywhere
-            if (present[k]) orw[k] = (lane == wi) ? kSimpleZero : orw[k];
-        }
-        h = h32_step(h, kw);
-        if (X64) {
-          if ((wi & 3) == 0) x0 = xx_round(x0, tw);
-          else if ((wi & 3) == 1) x1 = xx_round(x1, tw);
-          else if ((wi & 3) == 2) x2 = xx_round(x2, tw);
-          else x3 = xx_round(x3, tw);
+            for (int k = 1; k < NC; k++)  // simplified classes see 0x01 bytes everywhere
+              if (present[k]) orw[k] = (lane == (wi & 63)) ? kSimpleZero : orw[k];
+          }
+          if (X64) {
+            const int xl = (2 * qq + e) & 3;
+            if (xl == 0) x0 = xx_round(x0, tw);
+            else if (xl == 1) x1 = xx_round(x1, tw);
+            else if (xl == 2) x2 = xx_round(x2, tw);
+            else x3 = xx_round(x3, tw);
+          }
         }
       }
-    }
-    if (lane < kTileWords) {
+      // every 64 words (512 B), or at the end of a 256-B tile: store the column ORs
+      if (((q + 2) & 31) == 0 || q + 2 == SLOTS) {
+        const int wbase = (2 * q) & ~63;
+        if (lane < min(64, WORDS)) {
 #pragma unroll
-      for (int k = 0; k < NC; k++)
-        if (present[k])
-          *(uint64_t *)(a.chunk_or + ((size_t)chunk * NC + k) * a.map_size + (size_t)t * kTileW +
-                        lane * 8) = orw[k];
+          for (int k = 0; k < NC; k++)
+            if (present[k])
+              *(uint64_t *)(a.chunk_or + ((size_t)chunk * NC + k) * a.map_size +
+                            (size_t)t * TW + (size_t)(wbase + lane) * 8) = orw[k];
+        }
+#pragma unroll
+        for (int k = 0; k < NC; k++) orw[k] = 0;
+      }
     }
     __syncthreads();
   }
@@ -242,6 +274,204 @@ __global__ __launch_bounds__(64) void k_pass1(Pass1Args a) {
       a.shard_last[0] = h32;
       a.shard_last[1] = 1;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// pass 1, split form: two waves per 64-trace chunk sharing two 16-KiB LDS tile buffers.
+//   wave L (loader/chain): global loads two tiles ahead (registers), fills the LDS tile, and
+//          runs the serial per-trace chains (hash32 mix+step, optional XXH64) over the tile
+//          that wave T has transformed;
+//   wave T (transform):    per word, transform (classify/simplify) in place, per-class column
+//          OR across the 64 traces (DPP), DynamoRIO equality with the previous trace.
+// Step s: L chains tile s-1 and refills that buffer with tile s+1; T transforms tile s; one
+// barrier per step.  Two waves per chunk -> 2 waves per SIMD at 65,536 traces.
+// Raw zero words are left as 0 in LDS; a simplified trace's transformed word is never 0, so L
+// recognises an untouched zero word of a simplified lane and uses 0x0101010101010101.
+// ---------------------------------------------------------------------------------------------
+template <int MODE, bool IGN, bool X64>
+__global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
+  constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
+  constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = 16;  // 16 x 1-KiB loads per tile
+  // 2 tile buffers (32 KiB) + 8 KiB pad: at most 4 chunks per CU, so 1,024 chunks spread
+  // over all 256 CUs
+  __shared__ uint4 lds[2 * kChunk * SLOTS + 512];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const uint32_t chunk = blockIdx.x;
+  const uint64_t row0 = (uint64_t)chunk * kChunk;
+  const int nrows = (int)min((uint64_t)kChunk, (uint64_t)a.n - row0);
+  const bool valid = lane < nrows;
+  const int oc = (valid && a.outcome) ? a.outcome[row0 + lane] : KBZ_FUZZ_NONE;
+  const int cls = class_of(MODE, oc);
+  const int xf = valid ? class_xf(MODE, cls) : XF_RAW;
+  const bool simp = (xf == XF_SIMPLIFY);
+  const uint32_t ntiles = a.map_size / TW;
+
+  if (wave == 0) {
+    // ------------------------------------------------------------------ wave L
+    const int lr = lane / SLOTS, ls = lane % SLOTS;
+    const uint8_t *lbase = a.traces + row0 * a.stride + ls * 16;
+    // rows past the end of a partial chunk re-read its last row: those lanes are invalid and
+    // never contribute (T masks them out of the ORs; their hashes are not stored)
+    uint32_t roff[NLD];  // < 64 rows x stride: fits 32 bits (map_size <= 16 MiB)
+#pragma unroll
+    for (int i = 0; i < NLD; i++) roff[i] = (uint32_t)(min(RPI * i + lr, nrows - 1) * a.stride);
+    auto load_tile = [&](uint4 (&r)[NLD], uint32_t t) {
+      t = min(t, ntiles - 1);  // past the end: harmless re-read of the last tile
+      const uint8_t *p = lbase + (size_t)t * TW;
+#pragma unroll
+      for (int i = 0; i < NLD; i++) r[i] = ld_stream16(p + roff[i]);
+    };
+    auto store_tile = [&](const uint4 (&r)[NLD], int b) {
+#pragma unroll
+      for (int i = 0; i < NLD; i++) {
+        const int rr = RPI * i + lr;
+        lds[b * kChunk * SLOTS + rr * SLOTS + (ls ^ (rr & 15))] = r[i];
+      }
+    };
+    uint64_t h = (uint64_t)(kHashConst ^ a.map_size);
+    uint64_t x0 = kXP1 + kXP2, x1 = kXP2, x2 = 0, x3 = 0 - kXP1;
+    const uint64_t ksimp = h32_mix(kSimpleZero);
+    auto chain_tile = [&](uint32_t t, int b) {
+      const uint64_t *ig = IGN ? (const uint64_t *)(a.ignore + (size_t)t * TW) : nullptr;
+#pragma unroll 1
+      for (int q = 0; q < SLOTS; q += 2) {
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++) {
+          const uint4 v = lds[b * kChunk * SLOTS + lane * SLOTS + ((q + qq) ^ (lane & 15))];
+#pragma unroll
+          for (int e = 0; e < 2; e++) {
+            const int wi = 2 * (q + qq) + e;
+            const uint64_t w = ld_u64(v, e);
+            uint64_t tw, k;
+            if (__ballot(w != 0)) {
+              tw = (simp && w == 0) ? kSimpleZero : w;
+              k = h32_mix(tw & (IGN ? ig[wi] : ~0ull));
+            } else {
+              tw = simp ? kSimpleZero : 0;
+              k = simp ? ksimp : 0;
+            }
+            h = h32_step(h, k);
+            if (X64) {
+              const int xl = (2 * qq + e) & 3;
+              if (xl == 0) x0 = xx_round(x0, tw);
+              else if (xl == 1) x1 = xx_round(x1, tw);
+              else if (xl == 2) x2 = xx_round(x2, tw);
+              else x3 = xx_round(x3, tw);
+            }
+          }
+        }
+      }
+    };
+    // tile t is staged in R[t & 1]; step s chains tile s-1, stores tile s+1 into the buffer
+    // it just chained and prefetches tile s+3.  Loads and stores are unconditional (past the
+    // last tile they re-read it / fill a buffer nobody reads) so the loop is straight-line
+    // VMEM code and keeps the compiler's counted vmcnt (two tiles in flight).
+    const uint32_t pairs = (ntiles + 1) / 2;
+    uint4 R0[NLD], R1[NLD];
+    load_tile(R0, 0);
+    load_tile(R1, 1);
+    store_tile(R0, 0);
+    load_tile(R0, 2);
+    __syncthreads();
+    store_tile(R1, 1);  // step 0
+    load_tile(R1, 3);
+    __syncthreads();
+    for (uint32_t pi = 0; pi < pairs; pi++) {
+      const uint32_t s = 2 * pi + 1;
+      chain_tile(s - 1, 0);  // s-1 < ntiles always
+      store_tile(R0, 0);
+      load_tile(R0, s + 3);
+      __syncthreads();
+      if (s < ntiles) chain_tile(s, 1);
+      store_tile(R1, 1);
+      load_tile(R1, s + 4);
+      __syncthreads();
+    }
+    if (valid) {
+      const uint32_t h32 = h32_final(h);
+      a.h32[row0 + lane] = h32;
+      if (X64 && a.x64) {
+        uint64_t xh = rotl64(x0, 1) + rotl64(x1, 7) + rotl64(x2, 12) + rotl64(x3, 18);
+        xh = xx_merge(xh, x0);
+        xh = xx_merge(xh, x1);
+        xh = xx_merge(xh, x2);
+        xh = xx_merge(xh, x3);
+        xh += a.map_size;
+        a.x64[row0 + lane] = xx_avalanche(xh);
+      }
+      if (row0 + lane == (uint64_t)a.n - 1) {
+        a.shard_last[0] = h32;
+        a.shard_last[1] = 1;
+      }
+    }
+  } else {
+    // ------------------------------------------------------------------ wave T
+    uint64_t present[NC];
+#pragma unroll
+    for (int k = 0; k < NC; k++) present[k] = __ballot(valid && cls == k);
+    if (lane == 0) {
+      uint8_t m = 0;
+#pragma unroll
+      for (int k = 0; k < NC; k++) m |= present[k] ? (1u << k) : 0u;
+      a.chunk_cls[chunk] = m;
+    }
+    uint64_t neq = 0;
+    __syncthreads();
+    const uint32_t steps = 2 * ((ntiles + 1) / 2) + 1;  // barrier count must match wave L
+    for (uint32_t s = 0; s < steps; s++) {
+      if (s < ntiles) {
+        const int b = s & 1;
+        const uint64_t *ig = IGN ? (const uint64_t *)(a.ignore + (size_t)s * TW) : nullptr;
+        uint64_t orw[NC];
+#pragma unroll
+        for (int k = 0; k < NC; k++) orw[k] = 0;
+#pragma unroll 2
+        for (int q = 0; q < SLOTS; q++) {
+          uint4 *slot = &lds[b * kChunk * SLOTS + lane * SLOTS + (q ^ (lane & 15))];
+          uint4 v = *slot;
+          bool dirty = false;
+#pragma unroll
+          for (int e = 0; e < 2; e++) {
+            const int wi = 2 * q + e;
+            const uint64_t x = ld_u64(v, e);
+            if (__ballot(x != 0)) {
+              const uint64_t tw = xform8(x, xf);
+              if (e) { v.z = (uint32_t)tw; v.w = (uint32_t)(tw >> 32); }
+              else { v.x = (uint32_t)tw; v.y = (uint32_t)(tw >> 32); }
+              dirty = true;
+#pragma unroll
+              for (int k = 0; k < NC; k++) {
+                if (present[k]) {
+                  const uint64_t r = wave_or64((valid && cls == k) ? tw : 0);
+                  orw[k] = (lane == wi) ? r : orw[k];
+                }
+              }
+              if (MODE == KBZ_MODE_DYNAMORIO) {
+                const uint64_t rel = IGN ? ~nonzero_bytes8(ig[wi]) : ~0ull;
+                neq |= (tw ^ from_prev_lane(tw)) & rel;
+              }
+            } else if (MODE != KBZ_MODE_DYNAMORIO) {
+#pragma unroll
+              for (int k = 1; k < NC; k++)  // simplified classes see 0x01 bytes everywhere
+                if (present[k]) orw[k] = (lane == wi) ? kSimpleZero : orw[k];
+            }
+          }
+          if (MODE != KBZ_MODE_AFL && dirty) *slot = v;  // raw AFL words are their own transform
+          else if (MODE == KBZ_MODE_AFL && dirty && simp) *slot = v;
+        }
+        if (lane < TW / 8) {
+#pragma unroll
+          for (int k = 0; k < NC; k++)
+            if (present[k])
+              *(uint64_t *)(a.chunk_or + ((size_t)chunk * NC + k) * a.map_size +
+                            (size_t)s * TW + (size_t)lane * 8) = orw[k];
+        }
+      }
+      __syncthreads();
+    }
+    if (MODE == KBZ_MODE_DYNAMORIO && valid) a.neq[row0 + lane] = neq != 0;
   }
 }
 
@@ -675,7 +905,18 @@ void free_ctx(kbz_ctx *c) {
 
 template <int MODE, bool IGN, bool X64>
 void launch_pass1(const Pass1Args &a, uint32_t chunks, hipStream_t s) {
-  hipLaunchKernelGGL((k_pass1<MODE, IGN, X64>), dim3(chunks), dim3(64), 0, s, a);
+  static const int split = [] {
+    const char *e = getenv("KBZ_PASS1");
+    return e ? atoi(e) : 1;
+  }();
+  if (split) {
+    hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64>), dim3(chunks), dim3(128), 0, s, a);
+    return;
+  }
+  if (a.map_size % 512 == 0)
+    hipLaunchKernelGGL((k_pass1<MODE, IGN, X64, 512>), dim3(chunks), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_pass1<MODE, IGN, X64, 256>), dim3(chunks), dim3(64), 0, s, a);
 }
 
 int pass1_dispatch(kbz_ctx *c, const Pass1Args &a, uint32_t chunks, bool x64, hipStream_t s) {
@@ -704,6 +945,7 @@ int pass1_dispatch(kbz_ctx *c, const Pass1Args &a, uint32_t chunks, bool x64, hi
 int check_rows(const void *p, size_t stride, size_t M) {
   if (((uintptr_t)p & 15) || (stride & 15) || stride < M)
     return fail("traces must be 16-byte aligned with stride % 16 == 0 and stride >= map_size");
+  if (stride > (1u << 25)) return fail("stride must be <= 32 MiB");
   return 0;
 }
 

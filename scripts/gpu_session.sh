@@ -37,6 +37,15 @@ for s in $STEPS; do
       timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc2 -o run \
         -- python3 bench.py --steps 3 --warmup 1 --no-cpu ${BENCH_ARGS:-} > $OUT/pmc2.log 2>&1
       rc=$?; tail -2 $OUT/pmc2.log; [ $rc -eq 0 ] || exit $rc ;;
+    sq)
+      echo "== rocprofv3 SQ counters $(date +%T)"
+      timeout -k 10 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
+        --output-format csv -d $OUT/sq -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ${BENCH_ARGS:-} > $OUT/sq.log 2>&1
+      rc=$?; tail -2 $OUT/sq.log; [ $rc -eq 0 ] || exit $rc ;;
+    probe)
+      echo "== bwprobe $(date +%T)"
+      timeout -k 10 120 ./tools/bwprobe 4096 > $OUT/bwprobe.log 2>&1
+      rc=$?; cat $OUT/bwprobe.log; [ $rc -eq 0 ] || exit $rc ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
