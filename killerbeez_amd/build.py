@@ -39,8 +39,9 @@ def hipcc() -> str:
 
 def build_hip(force: bool = False, verbose: bool = False) -> str:
     if force or _stale(HIP_LIB, HIP_SOURCES + HIP_HEADERS):
+        extra = os.environ.get("KBZ_HIPCC_FLAGS", "").split()
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-Wall", "-Wno-unused-function", "-I", INC, "-I", CSRC, *HIP_SOURCES,
+               "-Wall", "-Wno-unused-function", "-I", INC, "-I", CSRC, *extra, *HIP_SOURCES,
                "-o", HIP_LIB + ".tmp"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)

@@ -40,8 +40,7 @@ namespace {
 
 constexpr int kChunk = 64;   // traces per chunk: one wave, one lane per trace
 constexpr int kTileW = 256;  // bytes of every row staged per tile
-constexpr int kTileWords = kTileW / 8;
-constexpr int kMaxSeg = 64;  // chunk segments for the column scan
+constexpr int kMaxSeg = 32;  // chunk segments for the column scan
 constexpr int kItemsPerCol = 8;
 
 enum { XF_RAW = 0, XF_CLASSIFY = 1, XF_SIMPLIFY = 2 };
@@ -79,12 +78,74 @@ __device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
 __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
   return (uint64_t)wave_or32((uint32_t)v) | ((uint64_t)wave_or32((uint32_t)(v >> 32)) << 32);
 }
-// value of lane-1 (lane 0 gets 0)
+// value of lane-1 (lane 0 gets 0): DPP wave_shr:1, no LDS round trip
 __device__ __forceinline__ uint64_t from_prev_lane(uint64_t v) {
-  const uint32_t lo = __shfl_up((uint32_t)v, 1), hi = __shfl_up((uint32_t)(v >> 32), 1);
+  const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)v, 0x138, 0xf, 0xf, false);
+  const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(v >> 32), 0x138, 0xf, 0xf, false);
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
+// hash32 chain step (afl_progs/hash.h:52-54) as 4 dependent instructions: xor, rotl 27 as two
+// v_alignbit (rotr 37), h*5 and +C as v_lshl_add_u64 (the compiler's default is two
+// quarter-rate v_mad_u64_u32 on the serial chain).
+__device__ __forceinline__ uint64_t h32_step_fast(uint64_t h, uint64_t k) {
+  const uint32_t lo = (uint32_t)h ^ (uint32_t)k, hi = (uint32_t)(h >> 32) ^ (uint32_t)(k >> 32);
+  const uint32_t rl = __builtin_amdgcn_alignbit(lo, hi, 5);
+  const uint32_t rh = __builtin_amdgcn_alignbit(hi, lo, 5);
+  uint64_t r = ((uint64_t)rh << 32) | rl, t;
+  const uint64_t c = 0x52dce729ull;
+  asm("v_lshl_add_u64 %0, %1, 2, %1" : "=v"(t) : "v"(r));
+  asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(t), "s"(c));
+  return r;
+}
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is also a release fence for
+// global memory: with vmcnt counting loads and stores in issue order, it drains this wave's
+// in-flight prefetch loads whenever a global store was issued after them.  Here only LDS
+// must be ordered: wait for this wave's LDS ops, then s_barrier ("memory" keeps the compiler
+// from moving memory accesses across it).
+// Prefetch loads issued as inline asm: the compiler does not track them, so the caller must
+// wait with vmcnt_wait<N>() before reading the registers (N = VMEM ops issued after them).
+// Used where the compiler's own counting would drain the prefetch (see k_pass1s).
+__device__ __forceinline__ void asm_load16(u32x4 &r, const uint8_t *p) {
+  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r) : "v"(p) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vmcnt_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// Drain every asm load, keeping their destination registers live up to the wait: an asm
+// load's output looks ready to the compiler, so once it is dead the compiler may reuse the
+// register while the load is still in flight (the late write would clobber it).
+template <int NL>
+__device__ __forceinline__ void drain_asm_loads(const u32x4 (&r0)[NL], const u32x4 (&r1)[NL]) {
+#pragma unroll
+  for (int i = 0; i < NL; i++) asm volatile("" ::"v"(r0[i]), "v"(r1[i]));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < NL; i++) asm volatile("" ::"v"(r0[i]), "v"(r1[i]));
+}
+// Diagnostic build only (-DKBZ_STAMPS): per-wave cycle accounting of pass 1's step phases,
+// read back by tools/stamps.py through kbz_debug_stamps().  No stamp executes otherwise.
+#ifdef KBZ_STAMPS
+__device__ unsigned long long g_kbz_stamps[4096 * 2 * 4];
+__device__ __forceinline__ unsigned long long stamp_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define KBZ_STAMP_DECL unsigned long long st_acc[4] = {0, 0, 0, 0}, st_t = stamp_now()
+#define KBZ_STAMP(i) do { const unsigned long long _n = stamp_now(); st_acc[i] += _n - st_t; st_t = _n; } while (0)
+#define KBZ_STAMP_FLUSH(slot) do { if ((threadIdx.x & 63) == 0 && (slot) < 8192) { for (int _i = 0; _i < 4; _i++) g_kbz_stamps[(slot) * 4 + _i] = st_acc[_i]; } } while (0)
+#else
+#define KBZ_STAMP_DECL do {} while (0)
+#define KBZ_STAMP(i) do {} while (0)
+#define KBZ_STAMP_FLUSH(slot) do {} while (0)
+#endif
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 // streaming 16-B load of data read exactly once (nontemporal: do not keep it in L2)
 __device__ __forceinline__ uint4 ld_stream16(const uint8_t *p) {
   const u32x4 v = __builtin_nontemporal_load((const u32x4 *)p);
@@ -118,184 +179,38 @@ struct Pass1Args {
   uint8_t *chunk_or;    // [chunks][nclass][map_size]
   uint8_t *chunk_cls;   // [chunks] bitmask of classes present
   uint32_t *shard_last; // [2]
+  uint8_t *segor;       // [nseg][nclass][map_size], zero on entry: OR'ed into with atomics
+  uint32_t seg_len;     // chunks per segment
 };
 
 // ---------------------------------------------------------------------------------------------
-// pass 1: one wave per chunk of 64 consecutive traces, lane = trace.
-// Each tile stages TW bytes of all 64 rows in LDS (TW = 512: 32 KiB, loaded as 32 coalesced
-// 1-KiB wave-instructions and kept in flight in registers while the previous tile is processed).
-// 16-B slot q of row r lives at slot q ^ (r & 15): the fill (2 rows per wave-instruction,
-// ds_write_b128) and the row-per-lane ds_read_b128 are both bank-conflict-free.
+// pass 1: two waves per 64-trace chunk (lane = trace) sharing two 16-KiB LDS tile buffers.
+// Both waves stream: each loads half of every tile's rows (8 x 1-KiB coalesced wave-loads per
+// tile), two tiles ahead in registers.  A single loader wave per chunk cannot keep enough
+// loads in flight (tools/patprobe: ~4.5 TB/s vs ~6.6 TB/s with two).
+//   wave L: fills rows 0-31 of tile s+1, runs the serial per-trace chains (hash32 mix+step,
+//           optional XXH64) over tile s-1 after wave T transformed it;
+//   wave T: fills rows 32-63 of tile s, then per word transforms it in place (classify /
+//           simplify), ORs each column over the 64 traces (DPP), DynamoRIO equality with the
+//           previous trace; stores the chunk's column ORs and ORs them into the segment
+//           aggregate (64-bit atomics, nonzero words only).
+// Step s (one barrier per step): T fills+transforms tile s in buffer s&1 while L chains tile
+// s-1 and then refills that buffer with its half of tile s+1.  16-B slot q of row r lives at
+// slot q ^ (r & 15): fills (ds_write_b128, 4 rows per instruction) and the row-per-lane
+// ds_read_b128 are both bank-conflict-free.  Raw zero words stay 0 in LDS; a simplified
+// trace's transformed word is never 0, so L maps an untouched 0 of a simplified lane to
+// 0x0101010101010101.
+// ABL (timing-only ablation builds, never used for results): 1 = T skips its per-word work,
+// 2 = L skips its chains, 3 = both.
 // ---------------------------------------------------------------------------------------------
-template <int MODE, bool IGN, bool X64, int TW>
-__global__ __launch_bounds__(64) void k_pass1(Pass1Args a) {
-  constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
-  constexpr int SLOTS = TW / 16;          // 16-B slots per row
-  constexpr int RPI = 64 / SLOTS;         // rows per wave-instruction (1 KiB each)
-  constexpr int NLD = 64 / RPI;           // loads per lane per tile
-  constexpr int WORDS = TW / 8;
-  __shared__ uint4 lds[kChunk * SLOTS];
-  const int lane = threadIdx.x;
-  const uint32_t chunk = blockIdx.x;
-  const uint64_t row0 = (uint64_t)chunk * kChunk;
-  const int nrows = (int)min((uint64_t)kChunk, (uint64_t)a.n - row0);
-  const bool valid = lane < nrows;
-  const int oc = (valid && a.outcome) ? a.outcome[row0 + lane] : KBZ_FUZZ_NONE;
-  const int cls = class_of(MODE, oc);
-  const int xf = valid ? class_xf(MODE, cls) : XF_RAW;
-  const bool simp = (xf == XF_SIMPLIFY);
-  uint64_t present[NC];
-#pragma unroll
-  for (int k = 0; k < NC; k++) present[k] = __ballot(valid && cls == k);
-  if (lane == 0) {
-    uint8_t m = 0;
-#pragma unroll
-    for (int k = 0; k < NC; k++) m |= present[k] ? (1u << k) : 0u;
-    a.chunk_cls[chunk] = m;
-  }
-
-  const int lr = lane / SLOTS, ls = lane % SLOTS;
-  const uint32_t ntiles = a.map_size / TW;
-  // row this lane loads in instruction i is RPI*i + lr; rows past the end of a partial
-  // chunk re-read the last valid row and are zeroed (no per-load branches)
-  const uint8_t *lbase = a.traces + row0 * a.stride + ls * 16;
-  uint4 buf[NLD];
-  auto load_tile = [&](uint32_t t) {
-    const uint8_t *p = lbase + (size_t)t * TW;
-    if (nrows == kChunk) {
-#pragma unroll
-      for (int i = 0; i < NLD; i++)
-        buf[i] = ld_stream16(p + (size_t)(RPI * i + lr) * a.stride);
-    } else {
-#pragma unroll
-      for (int i = 0; i < NLD; i++) {
-        const int r = RPI * i + lr;
-        const uint4 v = *(const uint4 *)(p + (size_t)min(r, nrows - 1) * a.stride);
-        buf[i] = r < nrows ? v : make_uint4(0, 0, 0, 0);
-      }
-    }
-  };
-
-  uint64_t h = (uint64_t)(kHashConst ^ a.map_size);
-  uint64_t x0 = kXP1 + kXP2, x1 = kXP2, x2 = 0, x3 = 0 - kXP1;  // XXH64 lanes, seed 0
-  uint64_t neq = 0;
-  const uint64_t ksimp = h32_mix(kSimpleZero);
-
-  load_tile(0);
-  for (uint32_t t = 0; t < ntiles; t++) {
-#pragma unroll
-    for (int i = 0; i < NLD; i++) {
-      const int r = RPI * i + lr;
-      lds[r * SLOTS + (ls ^ (r & 15))] = buf[i];
-    }
-    __syncthreads();
-    if (t + 1 < ntiles) load_tile(t + 1);
-
-    const uint64_t *ig = IGN ? (const uint64_t *)(a.ignore + (size_t)t * TW) : nullptr;
-    uint64_t orw[NC];
-#pragma unroll
-    for (int k = 0; k < NC; k++) orw[k] = 0;
-    // 2 slots = 4 words per iteration: XXH64 lane (word & 3) stays a compile-time index
-#pragma unroll 1
-    for (int q = 0; q < SLOTS; q += 2) {
-#pragma unroll
-      for (int qq = 0; qq < 2; qq++) {
-        const uint4 v = lds[lane * SLOTS + ((q + qq) ^ (lane & 15))];
-#pragma unroll
-        for (int e = 0; e < 2; e++) {
-          const int wi = 2 * (q + qq) + e;  // word index inside the tile
-          const uint64_t x = ld_u64(v, e);
-          uint64_t tw;
-          if (__ballot(x != 0)) {
-            tw = xform8(x, xf);
-            const uint64_t ignw = IGN ? ig[wi] : ~0ull;
-            h = h32_step(h, h32_mix(tw & ignw));
-#pragma unroll
-            for (int k = 0; k < NC; k++) {
-              if (present[k]) {
-                const uint64_t r = wave_or64((valid && cls == k) ? tw : 0);
-                orw[k] = (lane == (wi & 63)) ? r : orw[k];
-              }
-            }
-            if (MODE == KBZ_MODE_DYNAMORIO) {
-              const uint64_t rel = IGN ? ~nonzero_bytes8(ignw) : ~0ull;
-              neq |= (tw ^ from_prev_lane(tw)) & rel;
-            }
-          } else if (MODE == KBZ_MODE_DYNAMORIO) {
-            tw = 0;
-            h = rotl64(h, 27) * 5 + 0x52dce729;  // h32_step(h, 0)
-          } else {
-            tw = simp ? kSimpleZero : 0;
-            h = h32_step(h, simp ? ksimp : 0);
-#pragma unroll
-            for (int k = 1; k < NC; k++)  // simplified classes see 0x01 bytes everywhere
-              if (present[k]) orw[k] = (lane == (wi & 63)) ? kSimpleZero : orw[k];
-          }
-          if (X64) {
-            const int xl = (2 * qq + e) & 3;
-            if (xl == 0) x0 = xx_round(x0, tw);
-            else if (xl == 1) x1 = xx_round(x1, tw);
-            else if (xl == 2) x2 = xx_round(x2, tw);
-            else x3 = xx_round(x3, tw);
-          }
-        }
-      }
-      // every 64 words (512 B), or at the end of a 256-B tile: store the column ORs
-      if (((q + 2) & 31) == 0 || q + 2 == SLOTS) {
-        const int wbase = (2 * q) & ~63;
-        if (lane < min(64, WORDS)) {
-#pragma unroll
-          for (int k = 0; k < NC; k++)
-            if (present[k])
-              *(uint64_t *)(a.chunk_or + ((size_t)chunk * NC + k) * a.map_size +
-                            (size_t)t * TW + (size_t)(wbase + lane) * 8) = orw[k];
-        }
-#pragma unroll
-        for (int k = 0; k < NC; k++) orw[k] = 0;
-      }
-    }
-    __syncthreads();
-  }
-
-  if (valid) {
-    const uint32_t h32 = h32_final(h);
-    a.h32[row0 + lane] = h32;
-    if (MODE == KBZ_MODE_DYNAMORIO) a.neq[row0 + lane] = neq != 0;
-    if (X64 && a.x64) {
-      uint64_t xh = rotl64(x0, 1) + rotl64(x1, 7) + rotl64(x2, 12) + rotl64(x3, 18);
-      xh = xx_merge(xh, x0);
-      xh = xx_merge(xh, x1);
-      xh = xx_merge(xh, x2);
-      xh = xx_merge(xh, x3);
-      xh += a.map_size;
-      a.x64[row0 + lane] = xx_avalanche(xh);
-    }
-    if (row0 + lane == (uint64_t)a.n - 1) {
-      a.shard_last[0] = h32;
-      a.shard_last[1] = 1;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// pass 1, split form: two waves per 64-trace chunk sharing two 16-KiB LDS tile buffers.
-//   wave L (loader/chain): global loads two tiles ahead (registers), fills the LDS tile, and
-//          runs the serial per-trace chains (hash32 mix+step, optional XXH64) over the tile
-//          that wave T has transformed;
-//   wave T (transform):    per word, transform (classify/simplify) in place, per-class column
-//          OR across the 64 traces (DPP), DynamoRIO equality with the previous trace.
-// Step s: L chains tile s-1 and refills that buffer with tile s+1; T transforms tile s; one
-// barrier per step.  Two waves per chunk -> 2 waves per SIMD at 65,536 traces.
-// Raw zero words are left as 0 in LDS; a simplified trace's transformed word is never 0, so L
-// recognises an untouched zero word of a simplified lane and uses 0x0101010101010101.
-// ---------------------------------------------------------------------------------------------
-template <int MODE, bool IGN, bool X64>
+template <int MODE, bool IGN, bool X64, int ABL = 0>
 __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
-  constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = 16;  // 16 x 1-KiB loads per tile
+  constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = 8;  // 8 x 1-KiB loads per wave per tile
+  constexpr int TILE = kChunk * SLOTS;                     // uint4 per tile buffer
   // 2 tile buffers (32 KiB) + 8 KiB pad: at most 4 chunks per CU, so 1,024 chunks spread
   // over all 256 CUs
-  __shared__ uint4 lds[2 * kChunk * SLOTS + 512];
+  __shared__ uint4 lds[2 * TILE + 512];
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const uint32_t chunk = blockIdx.x;
@@ -307,39 +222,59 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   const int xf = valid ? class_xf(MODE, cls) : XF_RAW;
   const bool simp = (xf == XF_SIMPLIFY);
   const uint32_t ntiles = a.map_size / TW;
+  const uint32_t pairs = (ntiles + 1) / 2;
+
+  // this wave's half of the rows: rows past the end of a partial chunk re-read its last row
+  // (those lanes are invalid: masked out of the ORs, hashes not stored)
+  const int lr = lane / SLOTS, ls = lane % SLOTS;
+  const uint8_t *lbase = a.traces + row0 * a.stride + ls * 16;
+  uint32_t roff[NLD];  // < 64 rows x stride <= 32 MiB: fits 32 bits
+#pragma unroll
+  for (int i = 0; i < NLD; i++)
+    roff[i] = (uint32_t)(min(32 * wave + RPI * i + lr, nrows - 1) * a.stride);
+  // Prefetch: asm loads, waited for by hand (vmcnt counts VMEM ops of this wave in issue
+  // order).  Wave L issues no other VMEM op in its loop: at each fill the only younger ops
+  // are the other buffer's 8 loads -> vmcnt(8).  Wave T prefetches before transforming and
+  // every transform issues >= 1 global store, so at each loop fill >= 9 younger ops exist
+  // -> vmcnt(9); its first fill (prologue) has exactly the other buffer's 8 -> vmcnt(8).
+  auto load_half = [&](u32x4 (&r)[NLD], uint32_t t) {
+    t = min(t, ntiles - 1);  // past the end: harmless re-read of the last tile
+    const uint8_t *p = lbase + (size_t)t * TW;
+#pragma unroll
+    for (int i = 0; i < NLD; i++) asm_load16(r[i], p + roff[i]);
+  };
+  auto store_half = [&](const u32x4 (&r)[NLD], int b) {
+#pragma unroll
+    for (int i = 0; i < NLD; i++) {
+      const int rr = 32 * wave + RPI * i + lr;
+      const u32x4 v = r[i];
+      lds[b * TILE + rr * SLOTS + (ls ^ (rr & 15))] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  };
+  u32x4 R0[NLD], R1[NLD];
 
   if (wave == 0) {
     // ------------------------------------------------------------------ wave L
-    const int lr = lane / SLOTS, ls = lane % SLOTS;
-    const uint8_t *lbase = a.traces + row0 * a.stride + ls * 16;
-    // rows past the end of a partial chunk re-read its last row: those lanes are invalid and
-    // never contribute (T masks them out of the ORs; their hashes are not stored)
-    uint32_t roff[NLD];  // < 64 rows x stride: fits 32 bits (map_size <= 16 MiB)
-#pragma unroll
-    for (int i = 0; i < NLD; i++) roff[i] = (uint32_t)(min(RPI * i + lr, nrows - 1) * a.stride);
-    auto load_tile = [&](uint4 (&r)[NLD], uint32_t t) {
-      t = min(t, ntiles - 1);  // past the end: harmless re-read of the last tile
-      const uint8_t *p = lbase + (size_t)t * TW;
-#pragma unroll
-      for (int i = 0; i < NLD; i++) r[i] = ld_stream16(p + roff[i]);
-    };
-    auto store_tile = [&](const uint4 (&r)[NLD], int b) {
-#pragma unroll
-      for (int i = 0; i < NLD; i++) {
-        const int rr = RPI * i + lr;
-        lds[b * kChunk * SLOTS + rr * SLOTS + (ls ^ (rr & 15))] = r[i];
-      }
-    };
     uint64_t h = (uint64_t)(kHashConst ^ a.map_size);
     uint64_t x0 = kXP1 + kXP2, x1 = kXP2, x2 = 0, x3 = 0 - kXP1;
     const uint64_t ksimp = h32_mix(kSimpleZero);
     auto chain_tile = [&](uint32_t t, int b) {
+      if (ABL & 2) {
+        asm volatile("" ::"v"(lds[b * TILE + lane].x));
+        return;
+      }
       const uint64_t *ig = IGN ? (const uint64_t *)(a.ignore + (size_t)t * TW) : nullptr;
+      const uint4 *row = &lds[b * TILE + lane * SLOTS];
+      const int sw = lane & 15;
+      uint4 v0 = row[0 ^ sw], v1 = row[1 ^ sw];
 #pragma unroll 1
       for (int q = 0; q < SLOTS; q += 2) {
+        // software pipeline: the next two slots are in flight while these 4 words chain
+        const int qn = (q + 2) & (SLOTS - 1);
+        const uint4 n0 = row[qn ^ sw], n1 = row[(qn + 1) ^ sw];
 #pragma unroll
         for (int qq = 0; qq < 2; qq++) {
-          const uint4 v = lds[b * kChunk * SLOTS + lane * SLOTS + ((q + qq) ^ (lane & 15))];
+          const uint4 v = qq ? v1 : v0;
 #pragma unroll
           for (int e = 0; e < 2; e++) {
             const int wi = 2 * (q + qq) + e;
@@ -352,7 +287,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
               tw = simp ? kSimpleZero : 0;
               k = simp ? ksimp : 0;
             }
-            h = h32_step(h, k);
+            h = h32_step_fast(h, k);
             if (X64) {
               const int xl = (2 * qq + e) & 3;
               if (xl == 0) x0 = xx_round(x0, tw);
@@ -362,33 +297,47 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
             }
           }
         }
+        v0 = n0;
+        v1 = n1;
       }
     };
-    // tile t is staged in R[t & 1]; step s chains tile s-1, stores tile s+1 into the buffer
-    // it just chained and prefetches tile s+3.  Loads and stores are unconditional (past the
-    // last tile they re-read it / fill a buffer nobody reads) so the loop is straight-line
-    // VMEM code and keeps the compiler's counted vmcnt (two tiles in flight).
-    const uint32_t pairs = (ntiles + 1) / 2;
-    uint4 R0[NLD], R1[NLD];
-    load_tile(R0, 0);
-    load_tile(R1, 1);
-    store_tile(R0, 0);
-    load_tile(R0, 2);
-    __syncthreads();
-    store_tile(R1, 1);  // step 0
-    load_tile(R1, 3);
-    __syncthreads();
+    // L's half of tile t is staged in R[t & 1].  Step s: chain tile s-1, store own half of
+    // tile s+1 into the buffer just chained, prefetch own half of tile s+3.  Loads/stores are
+    // unconditional (straight-line VMEM code keeps the compiler's counted vmcnt).
+    load_half(R0, 0);
+    load_half(R1, 1);
+    vmcnt_wait<NLD>();
+    store_half(R0, 0);
+    load_half(R0, 2);
+    lds_barrier();  // (A) L's half of tile 0 is in buffer 0
+    vmcnt_wait<NLD>();
+    store_half(R1, 1);  // step 0
+    load_half(R1, 3);
+    lds_barrier();
+    KBZ_STAMP_DECL;
     for (uint32_t pi = 0; pi < pairs; pi++) {
       const uint32_t s = 2 * pi + 1;
-      chain_tile(s - 1, 0);  // s-1 < ntiles always
-      store_tile(R0, 0);
-      load_tile(R0, s + 3);
-      __syncthreads();
+      chain_tile(s - 1, 0);
+      KBZ_STAMP(0);
+      vmcnt_wait<NLD>();
+      KBZ_STAMP(1);
+      store_half(R0, 0);
+      load_half(R0, s + 3);
+      KBZ_STAMP(2);
+      lds_barrier();
+      KBZ_STAMP(3);
       if (s < ntiles) chain_tile(s, 1);
-      store_tile(R1, 1);
-      load_tile(R1, s + 4);
-      __syncthreads();
+      KBZ_STAMP(0);
+      vmcnt_wait<NLD>();
+      KBZ_STAMP(1);
+      store_half(R1, 1);
+      load_half(R1, s + 4);
+      KBZ_STAMP(2);
+      lds_barrier();
+      KBZ_STAMP(3);
     }
+    KBZ_STAMP_FLUSH(chunk * 2 + 0);
+    drain_asm_loads(R0, R1);
     if (valid) {
       const uint32_t h32 = h32_final(h);
       a.h32[row0 + lane] = h32;
@@ -418,59 +367,98 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
       a.chunk_cls[chunk] = m;
     }
     uint64_t neq = 0;
-    __syncthreads();
-    const uint32_t steps = 2 * ((ntiles + 1) / 2) + 1;  // barrier count must match wave L
-    for (uint32_t s = 0; s < steps; s++) {
-      if (s < ntiles) {
-        const int b = s & 1;
-        const uint64_t *ig = IGN ? (const uint64_t *)(a.ignore + (size_t)s * TW) : nullptr;
-        uint64_t orw[NC];
+    const uint32_t seg = chunk / a.seg_len;
+    auto transform_tile = [&](uint32_t s) {
+      const int b = s & 1;
+      const uint64_t *ig = IGN ? (const uint64_t *)(a.ignore + (size_t)s * TW) : nullptr;
+      uint64_t orw[NC];
 #pragma unroll
-        for (int k = 0; k < NC; k++) orw[k] = 0;
+      for (int k = 0; k < NC; k++) orw[k] = 0;
+      uint4 *row = &lds[b * TILE + lane * SLOTS];
+      const int sw = lane & 15;
+      uint4 vnext = row[0 ^ sw];
 #pragma unroll 2
-        for (int q = 0; q < SLOTS; q++) {
-          uint4 *slot = &lds[b * kChunk * SLOTS + lane * SLOTS + (q ^ (lane & 15))];
-          uint4 v = *slot;
-          bool dirty = false;
+      for (int q = 0; q < ((ABL & 1) ? 0 : SLOTS); q++) {
+        uint4 *slot = &row[q ^ sw];
+        uint4 v = vnext;
+        vnext = row[((q + 1) & (SLOTS - 1)) ^ sw];  // next slot in flight meanwhile
+        bool dirty = false;
 #pragma unroll
-          for (int e = 0; e < 2; e++) {
-            const int wi = 2 * q + e;
-            const uint64_t x = ld_u64(v, e);
-            if (__ballot(x != 0)) {
-              const uint64_t tw = xform8(x, xf);
-              if (e) { v.z = (uint32_t)tw; v.w = (uint32_t)(tw >> 32); }
-              else { v.x = (uint32_t)tw; v.y = (uint32_t)(tw >> 32); }
-              dirty = true;
+        for (int e = 0; e < 2; e++) {
+          const int wi = 2 * q + e;
+          const uint64_t x = ld_u64(v, e);
+          if (__ballot(x != 0)) {
+            const uint64_t tw = xform8(x, xf);
+            if (e) { v.z = (uint32_t)tw; v.w = (uint32_t)(tw >> 32); }
+            else { v.x = (uint32_t)tw; v.y = (uint32_t)(tw >> 32); }
+            dirty = true;
 #pragma unroll
-              for (int k = 0; k < NC; k++) {
-                if (present[k]) {
-                  const uint64_t r = wave_or64((valid && cls == k) ? tw : 0);
-                  orw[k] = (lane == wi) ? r : orw[k];
-                }
+            for (int k = 0; k < NC; k++) {
+              if (present[k]) {
+                const uint64_t r = wave_or64((valid && cls == k) ? tw : 0);
+                orw[k] = (lane == wi) ? r : orw[k];
               }
-              if (MODE == KBZ_MODE_DYNAMORIO) {
-                const uint64_t rel = IGN ? ~nonzero_bytes8(ig[wi]) : ~0ull;
-                neq |= (tw ^ from_prev_lane(tw)) & rel;
-              }
-            } else if (MODE != KBZ_MODE_DYNAMORIO) {
-#pragma unroll
-              for (int k = 1; k < NC; k++)  // simplified classes see 0x01 bytes everywhere
-                if (present[k]) orw[k] = (lane == wi) ? kSimpleZero : orw[k];
             }
-          }
-          if (MODE != KBZ_MODE_AFL && dirty) *slot = v;  // raw AFL words are their own transform
-          else if (MODE == KBZ_MODE_AFL && dirty && simp) *slot = v;
-        }
-        if (lane < TW / 8) {
+            if (MODE == KBZ_MODE_DYNAMORIO) {
+              const uint64_t rel = IGN ? ~nonzero_bytes8(ig[wi]) : ~0ull;
+              neq |= (tw ^ from_prev_lane(tw)) & rel;
+            }
+          } else if (MODE != KBZ_MODE_DYNAMORIO) {
 #pragma unroll
-          for (int k = 0; k < NC; k++)
-            if (present[k])
-              *(uint64_t *)(a.chunk_or + ((size_t)chunk * NC + k) * a.map_size +
-                            (size_t)s * TW + (size_t)lane * 8) = orw[k];
+            for (int k = 1; k < NC; k++)  // simplified classes see 0x01 bytes everywhere
+              if (present[k]) orw[k] = (lane == wi) ? kSimpleZero : orw[k];
+          }
         }
+        // raw AFL words are their own transform (only simplified lanes change)
+        if (dirty && (MODE != KBZ_MODE_AFL || simp)) *slot = v;
       }
-      __syncthreads();
+      if (lane < TW / 8) {
+#pragma unroll
+        for (int k = 0; k < NC; k++)
+          if (present[k]) {
+            const size_t off = (size_t)k * a.map_size + (size_t)s * TW + (size_t)lane * 8;
+            *(uint64_t *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) = orw[k];
+            // segment aggregate: most words are 0 (no atomic); hot words collide seg_len-way
+            if (orw[k])
+              atomicOr((unsigned long long *)(a.segor + (size_t)seg * NC * a.map_size + off),
+                       (unsigned long long)orw[k]);
+          }
+      }
+    };
+    // T's half of tile t is staged in R[t & 1].  Step s: store own half of tile s (L's half
+    // arrived before the previous barrier), prefetch own half of tile s+2, transform tile s.
+    load_half(R0, 0);
+    load_half(R1, 1);
+    lds_barrier();  // (A)
+    vmcnt_wait<NLD>();
+    store_half(R0, 0);
+    load_half(R0, 2);
+    transform_tile(0);
+    lds_barrier();
+    KBZ_STAMP_DECL;
+    for (uint32_t pi = 0; pi < pairs; pi++) {
+      const uint32_t s = 2 * pi + 1;
+      vmcnt_wait<NLD + 1>();
+      KBZ_STAMP(1);
+      store_half(R1, 1);
+      load_half(R1, s + 2);
+      KBZ_STAMP(2);
+      if (s < ntiles) transform_tile(s);
+      KBZ_STAMP(0);
+      lds_barrier();
+      KBZ_STAMP(3);
+      vmcnt_wait<NLD + 1>();
+      KBZ_STAMP(1);
+      store_half(R0, 0);
+      load_half(R0, s + 3);
+      KBZ_STAMP(2);
+      if (s + 1 < ntiles) transform_tile(s + 1);
+      KBZ_STAMP(0);
+      lds_barrier();
+      KBZ_STAMP(3);
     }
+    KBZ_STAMP_FLUSH(chunk * 2 + 1);
+    drain_asm_loads(R0, R1);
     if (MODE == KBZ_MODE_DYNAMORIO && valid) a.neq[row0 + lane] = neq != 0;
   }
 }
@@ -478,97 +466,87 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
 // DynamoRIO last-hash skip: skip[j] = hash[j] == hash[j-1] (hash[-1] = previous exec's).
 // A skipped trace must not touch the virgin map; pass 1 OR'ed it in, which is harmless only
 // when it equals its predecessor on the bytes has_new_bits looks at.  Otherwise its chunk is
-// flagged for recomputation.
+// queued (fix list) for recomputation without the skipped traces.
 __global__ void k_skip(const uint32_t *h32, const uint8_t *neq, uint32_t n,
                        const uint32_t *prev_last /*[2] or null*/, const uint32_t *ctx_last,
                        const uint32_t *global_last /*[2]*/, uint32_t *next_last,
-                       uint8_t *skip, uint8_t *flags) {
+                       uint8_t *skip, uint32_t *flags, uint32_t *fix_list, uint32_t *fix_cnt) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j == 0) {
-    *next_last = global_last[1] ? global_last[0] : *ctx_last;
-  }
+  if (j == 0) *next_last = global_last[1] ? global_last[0] : *ctx_last;
   if (j >= n) return;
   uint32_t hp;
   if (j) hp = h32[j - 1];
   else hp = prev_last ? prev_last[0] : *ctx_last;
   const bool sk = h32[j] == hp;
   skip[j] = sk;
-  if (sk && ((j % kChunk) == 0 || neq[j])) flags[j / kChunk] = 1;
+  if (sk && ((j % kChunk) == 0 || neq[j])) {
+    const uint32_t c = j / kChunk;
+    if (atomicExch(&flags[c], 1u) == 0u) fix_list[atomicAdd(fix_cnt, 1u)] = c;
+  }
 }
 
-// Recompute chunk ORs (DynamoRIO class 0) without skipped traces for flagged chunks.
+// Recompute chunk ORs (DynamoRIO class 0) without skipped traces, for listed chunks.
 __global__ __launch_bounds__(256) void k_fixchunk(const uint8_t *traces, size_t stride, uint32_t n,
                                                    uint32_t map_size, const uint8_t *skip,
-                                                   const uint8_t *flags, uint8_t *chunk_or) {
-  const uint32_t chunk = blockIdx.y;
-  if (!flags[chunk]) return;
-  const uint32_t col = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
-  if (col >= map_size) return;
-  const uint64_t row0 = (uint64_t)chunk * kChunk;
-  const int nrows = (int)min((uint64_t)kChunk, (uint64_t)n - row0);
-  uint4 acc = make_uint4(0, 0, 0, 0);
-  for (int r = 0; r < nrows; r++) {
-    if (skip[row0 + r]) continue;
-    acc = or4(acc, classify16(*(const uint4 *)(traces + (row0 + r) * stride + col)));
+                                                   const uint32_t *fix_list,
+                                                   const uint32_t *fix_cnt, uint8_t *chunk_or) {
+  const uint32_t ncol = map_size / 16, cnt = *fix_cnt;
+  for (size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x; w < (size_t)cnt * ncol;
+       w += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t chunk = fix_list[w / ncol];
+    const uint32_t col = (uint32_t)(w % ncol) * 16;
+    const uint64_t row0 = (uint64_t)chunk * kChunk;
+    const int nrows = (int)min((uint64_t)kChunk, (uint64_t)n - row0);
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (int r = 0; r < nrows; r++) {
+      if (skip[row0 + r]) continue;
+      acc = or4(acc, classify16(*(const uint4 *)(traces + (row0 + r) * stride + col)));
+    }
+    *(uint4 *)(chunk_or + (size_t)chunk * map_size + col) = acc;
   }
-  *(uint4 *)(chunk_or + (size_t)chunk * map_size + col) = acc;
 }
 
-// segOR[s][k][:] = OR of chunk aggregates in segment s.
-__global__ __launch_bounds__(256) void k_segor(const uint8_t *chunk_or, const uint8_t *chunk_cls,
-                                                uint32_t nchunks, uint32_t seg_len, int nclass,
-                                                uint32_t map_size, uint8_t *segor) {
-  const uint32_t col = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
-  const uint32_t s = blockIdx.y;
-  const int k = blockIdx.z;
-  if (col >= map_size) return;
-  const uint32_t c0 = s * seg_len, c1 = min(nchunks, c0 + seg_len);
-  uint4 acc = make_uint4(0, 0, 0, 0);
-  for (uint32_t c = c0; c < c1; c++)
-    if ((chunk_cls[c] >> k) & 1)
-      acc = or4(acc, *(const uint4 *)(chunk_or + ((size_t)c * nclass + k) * map_size + col));
-  *(uint4 *)(segor + ((size_t)s * nclass + k) * map_size + col) = acc;
+// Recompute the segment aggregates of segments holding a listed chunk (idempotent).
+__global__ __launch_bounds__(256) void k_segfix(const uint8_t *chunk_or, const uint8_t *chunk_cls,
+                                                 uint32_t nchunks, uint32_t seg_len,
+                                                 uint32_t map_size, const uint32_t *fix_list,
+                                                 const uint32_t *fix_cnt, uint8_t *segor) {
+  const uint32_t ncol = map_size / 16, cnt = *fix_cnt;
+  for (size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x; w < (size_t)cnt * ncol;
+       w += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t seg = fix_list[w / ncol] / seg_len;
+    const uint32_t col = (uint32_t)(w % ncol) * 16;
+    const uint32_t c0 = seg * seg_len, c1 = min(nchunks, c0 + seg_len);
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (uint32_t c = c0; c < c1; c++)
+      if (chunk_cls[c] & 1) acc = or4(acc, *(const uint4 *)(chunk_or + (size_t)c * map_size + col));
+    *(uint4 *)(segor + (size_t)seg * map_size + col) = acc;
+  }
 }
 
-// total[k][:] = OR over segments.
-__global__ __launch_bounds__(256) void k_total(const uint8_t *segor, uint32_t nseg, int nclass,
-                                                uint32_t map_size, uint8_t *total) {
-  const uint32_t col = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
+// Per column (8 B per thread): segprev[s] = OR of segments < s (local exclusive prefix),
+// total = OR of all segments; segor is re-zeroed for the next batch.
+__global__ __launch_bounds__(256) void k_total(uint8_t *segor, uint32_t nseg, int nclass,
+                                                uint32_t map_size, uint8_t *segprev,
+                                                uint8_t *total) {
+  const uint32_t col = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
   const int k = blockIdx.z;
   if (col >= map_size) return;
-  uint4 acc = make_uint4(0, 0, 0, 0);
-  for (uint32_t s = 0; s < nseg; s++)
-    acc = or4(acc, *(const uint4 *)(segor + ((size_t)s * nclass + k) * map_size + col));
-  *(uint4 *)(total + (size_t)k * map_size + col) = acc;
-}
-
-// segprev = exclusive prefix over segments (seeded with the OR of earlier shards);
-// vnext = V & ~(OR of the whole batch) on the bytes has_new_bits may update.
-__global__ __launch_bounds__(256) void k_prefix(const uint8_t *segor, uint32_t nseg, int nclass,
-                                                 uint32_t map_size, const uint8_t *gprefix,
-                                                 const uint8_t *gtotal, const uint8_t *ignore,
-                                                 const uint8_t *vcur, uint8_t *vnext,
-                                                 uint8_t *segprev) {
-  const uint32_t col = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
-  const int k = blockIdx.z;
-  if (col >= map_size) return;
-  uint4 acc = gprefix ? *(const uint4 *)(gprefix + (size_t)k * map_size + col)
-                      : make_uint4(0, 0, 0, 0);
-  for (uint32_t s = 0; s < nseg; s++) {
-    *(uint4 *)(segprev + ((size_t)s * nclass + k) * map_size + col) = acc;
-    acc = or4(acc, *(const uint4 *)(segor + ((size_t)s * nclass + k) * map_size + col));
+  uint64_t v[kMaxSeg];
+#pragma unroll
+  for (int s = 0; s < kMaxSeg; s++)  // all loads in flight at once
+    v[s] = s < (int)nseg ? *(const uint64_t *)(segor + ((size_t)s * nclass + k) * map_size + col) : 0;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int s = 0; s < kMaxSeg; s++) {
+    if (s < (int)nseg) {
+      const size_t off = ((size_t)s * nclass + k) * map_size + col;
+      *(uint64_t *)(segprev + off) = acc;
+      *(uint64_t *)(segor + off) = 0;  // ready for the next batch
+      acc |= v[s];
+    }
   }
-  uint4 tot = *(const uint4 *)(gtotal + (size_t)k * map_size + col);
-  if (ignore) {  // has_new_bits_with_ignore never writes bytes whose ignore byte is nonzero
-    const uint4 ig = *(const uint4 *)(ignore + col);
-    const uint64_t m0 = nonzero_bytes8((uint64_t)ig.x | ((uint64_t)ig.y << 32));
-    const uint64_t m1 = nonzero_bytes8((uint64_t)ig.z | ((uint64_t)ig.w << 32));
-    tot.x &= ~(uint32_t)m0; tot.y &= ~(uint32_t)(m0 >> 32);
-    tot.z &= ~(uint32_t)m1; tot.w &= ~(uint32_t)(m1 >> 32);
-  }
-  const uint4 v = *(const uint4 *)(vcur + (size_t)k * map_size + col);
-  *(uint4 *)(vnext + (size_t)k * map_size + col) =
-      make_uint4(v.x & ~tot.x, v.y & ~tot.y, v.z & ~tot.z, v.w & ~tot.w);
+  *(uint64_t *)(total + (size_t)k * map_size + col) = acc;
 }
 
 // item: [7:0] new bits, [8] score-2 candidate, [10:9] class, [34:11] column, [63:35] chunk
@@ -578,44 +556,100 @@ __device__ __forceinline__ uint64_t pack_item(uint32_t chunk, int k, uint32_t co
          ((uint64_t)f2 << 8) | nb;
 }
 
+// Append this lane's claim items (one per nonzero byte of nb) with ONE atomic per wave:
+// wave-wide exclusive prefix of the per-lane counts, lane 63 reserves the block.
+__device__ __forceinline__ uint32_t wave_excl_prefix(uint32_t v, uint32_t &total) {
+  const int lane = threadIdx.x & 63;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  total = __shfl(x, 63);
+  return x - v;
+}
+__device__ __forceinline__ void emit_items_wave(uint32_t chunk, int k, uint32_t col, uint4 nb,
+                                                uint4 vir, uint4 prev, uint64_t *items,
+                                                uint32_t cap, uint32_t *counters) {
+  const uint32_t w[4] = {nb.x, nb.y, nb.z, nb.w};
+  const uint32_t vv[4] = {vir.x, vir.y, vir.z, vir.w};
+  const uint32_t pv[4] = {prev.x, prev.y, prev.z, prev.w};
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) cnt += __popc(nonzero_bytes8(w[i]) & 0x80808080u);
+  uint32_t total;
+  const uint32_t off = wave_excl_prefix(cnt, total);
+  uint32_t base = 0;
+  if ((threadIdx.x & 63) == 63) base = atomicAdd(&counters[0], total);
+  base = __shfl(base, 63) + off;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint32_t x = (w[i] >> (8 * b)) & 0xff;
+      if (!x) continue;
+      const bool f2 = ((vv[i] >> (8 * b)) & 0xff) == 0xff && ((pv[i] >> (8 * b)) & 0xff) == 0;
+      if (base < cap) items[base] = pack_item(chunk, k, col + 4 * i + b, x, f2);
+      else atomicOr(&counters[1], 1u);
+      base++;
+    }
+}
+
+// Per (segment, 16-B column group): walk the segment's chunks in order with the running OR
+// `prev` (seeded with the OR of earlier segments and earlier shards); bits a chunk adds
+// that are still virgin become claim items.  Blocks of segment 0 also write V' = V & ~total.
 __global__ __launch_bounds__(256) void k_scan(const uint8_t *chunk_or, const uint8_t *chunk_cls,
                                                uint32_t nchunks, uint32_t seg_len, int nclass,
                                                uint32_t map_size, const uint8_t *segprev,
-                                               const uint8_t *vcur, const uint8_t *ignore,
-                                               uint64_t *items, uint32_t cap, uint32_t *counters) {
-  const uint32_t col = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
+                                               const uint8_t *gprefix, const uint8_t *gtotal,
+                                               const uint8_t *vcur, uint8_t *vnext,
+                                               const uint8_t *ignore, uint64_t *items,
+                                               uint32_t cap, uint32_t *counters) {
+  // no early return: every lane of a wave takes part in the item-allocation prefix
+  const uint32_t col0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  const bool live = col0 < map_size;
+  const uint32_t col = live ? col0 : 0;
   const uint32_t s = blockIdx.y;
   const int k = blockIdx.z;
-  if (col >= map_size) return;
-  const uint32_t c0 = s * seg_len, c1 = min(nchunks, c0 + seg_len);
-  uint8_t prev[16], vir[16], rel[16];
-  {
-    const uint4 p = *(const uint4 *)(segprev + ((size_t)s * nclass + k) * map_size + col);
-    const uint4 v = *(const uint4 *)(vcur + (size_t)k * map_size + col);
-    memcpy(prev, &p, 16);
-    memcpy(vir, &v, 16);
-    if (ignore) {
-      const uint4 ig = *(const uint4 *)(ignore + col);
-      uint8_t igb[16];
-      memcpy(igb, &ig, 16);
-      for (int b = 0; b < 16; b++) rel[b] = igb[b] ? 0 : 0xff;
-    } else {
-      for (int b = 0; b < 16; b++) rel[b] = 0xff;
-    }
+  const size_t kc = (size_t)k * map_size + col;
+  uint4 prev = *(const uint4 *)(segprev + (size_t)s * nclass * map_size + kc);
+  if (gprefix) prev = or4(prev, *(const uint4 *)(gprefix + kc));
+  const uint4 vir = *(const uint4 *)(vcur + kc);
+  uint4 rel = make_uint4(~0u, ~0u, ~0u, ~0u);
+  if (ignore) {  // has_new_bits_with_ignore only examines bytes whose ignore byte is 0
+    const uint4 ig = *(const uint4 *)(ignore + col);
+    const uint64_t m0 = nonzero_bytes8((uint64_t)ig.x | ((uint64_t)ig.y << 32));
+    const uint64_t m1 = nonzero_bytes8((uint64_t)ig.z | ((uint64_t)ig.w << 32));
+    rel = make_uint4(~(uint32_t)m0, ~(uint32_t)(m0 >> 32), ~(uint32_t)m1, ~(uint32_t)(m1 >> 32));
   }
-  for (uint32_t c = c0; c < c1; c++) {
-    if (!((chunk_cls[c] >> k) & 1)) continue;
-    const uint4 o4 = *(const uint4 *)(chunk_or + ((size_t)c * nclass + k) * map_size + col);
-    uint8_t o[16];
-    memcpy(o, &o4, 16);
-    for (int b = 0; b < 16; b++) {
-      const uint32_t nb = o[b] & vir[b] & (uint8_t)~prev[b] & rel[b];
-      if (nb) {
-        const uint32_t idx = atomicAdd(&counters[0], 1u);
-        if (idx < cap) items[idx] = pack_item(c, k, col + b, nb, vir[b] == 0xff && prev[b] == 0);
-        else atomicOr(&counters[1], 1u);
-      }
-      prev[b] |= o[b];
+  if (s == 0 && live) {
+    const uint4 t = *(const uint4 *)(gtotal + kc);
+    *(uint4 *)(vnext + kc) = make_uint4(vir.x & ~(t.x & rel.x), vir.y & ~(t.y & rel.y),
+                                        vir.z & ~(t.z & rel.z), vir.w & ~(t.w & rel.w));
+  }
+  const uint4 vr = live ? make_uint4(vir.x & rel.x, vir.y & rel.y, vir.z & rel.z, vir.w & rel.w)
+                        : make_uint4(0, 0, 0, 0);
+  const uint32_t c0 = s * seg_len, c1 = min(nchunks, c0 + seg_len);
+  // 8 chunks per batch, loads issued unconditionally (a chunk without traces of class k has a
+  // stale row: masked to 0 after the load) so each batch costs one memory round trip
+  for (uint32_t cb = c0; cb < c1; cb += 8) {
+    uint4 o[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t c = min(cb + u, c1 - 1);
+      o[u] = *(const uint4 *)(chunk_or + (size_t)c * nclass * map_size + kc);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t c = cb + u;  // uniform across the block
+      if (c >= c1) break;
+      if (!((chunk_cls[c] >> k) & 1)) continue;
+      const uint4 nb = make_uint4(o[u].x & vr.x & ~prev.x, o[u].y & vr.y & ~prev.y,
+                                  o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
+      if (__ballot(nb.x | nb.y | nb.z | nb.w))  // wave-uniform: all lanes join the prefix
+        emit_items_wave(c, k, col, nb, vir, prev, items, cap, counters);
+      prev = or4(prev, o[u]);
     }
   }
 }
@@ -637,13 +671,12 @@ __global__ __launch_bounds__(256) void k_resolve(const uint8_t *traces, size_t s
     const uint32_t col = (item >> 11) & 0xffffff;
     const uint32_t chunk = (uint32_t)(item >> 35);
     const uint64_t row = (uint64_t)chunk * kChunk + lane;
-    bool ok = row < n;
-    if (ok) {
-      const int oc = outcome ? outcome[row] : KBZ_FUZZ_NONE;
-      ok = class_of(mode, oc) == k;
-      if (ok && skip) ok = !skip[row];
-    }
-    const uint32_t tb = ok ? byte_xform(traces[row * stride + col], class_xf(mode, k)) : 0u;
+    const uint64_t rc = min(row, (uint64_t)n - 1);  // independent loads, one round trip
+    const int oc = outcome ? outcome[rc] : KBZ_FUZZ_NONE;
+    const uint8_t sk = skip ? skip[rc] : 0;
+    const uint32_t raw = traces[rc * stride + col];
+    const bool ok = row < n && class_of(mode, oc) == k && !sk;
+    const uint32_t tb = ok ? byte_xform(raw, class_xf(mode, k)) : 0u;
     const uint64_t first_nz = __ballot(tb != 0);
     uint64_t claimers = 0;
     for (int b = 0; b < 8; b++) {
@@ -662,12 +695,13 @@ __global__ __launch_bounds__(256) void k_resolve(const uint8_t *traces, size_t s
   }
 }
 
-__global__ void k_pack(const uint32_t *hnb32, const uint32_t *h32, uint32_t n, uint8_t *hnb_out,
+__global__ void k_pack(uint32_t *hnb32, const uint32_t *h32, uint32_t n, uint8_t *hnb_out,
                        uint32_t *h32_out) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
-  hnb_out[j] = (uint8_t)hnb32[j];
+  if (hnb_out) hnb_out[j] = (uint8_t)hnb32[j];
   if (h32_out) h32_out[j] = h32[j];
+  hnb32[j] = 0;  // ready for the next batch
 }
 
 __global__ __launch_bounds__(256) void k_or_reduce(uint8_t *out, const uint8_t *in, size_t r_lo,
@@ -815,7 +849,8 @@ struct kbz_ctx {
   uint8_t *ignore = nullptr;
   uint8_t *chunk_or = nullptr;
   uint8_t *chunk_cls = nullptr;
-  uint8_t *flags = nullptr;
+  uint32_t *flags = nullptr;     // [chunks] queued for recomputation
+  uint32_t *fix_list = nullptr;  // [chunks]
   uint8_t *skip = nullptr;
   uint8_t *neq = nullptr;
   uint32_t *h32 = nullptr;
@@ -825,13 +860,14 @@ struct kbz_ctx {
   uint8_t *total = nullptr;
   uint64_t *items = nullptr;
   uint32_t item_cap = 0;
-  uint32_t *counters = nullptr;  // [0] items, [1] overflow, [2] resolve error
+  uint32_t *counters = nullptr;  // [0] items, [1] overflow, [2] resolve error, [3] fix list
   uint32_t *shard_last = nullptr;  // [2]
   // in-flight shard
   const uint8_t *cur_traces = nullptr;
   size_t cur_n = 0, cur_stride = 0;
   const int8_t *cur_outcome = nullptr;
   uint32_t *cur_h32_out = nullptr;
+  uint32_t *cur_h32 = nullptr;  // where pass 1 wrote this shard's hashes
   uint32_t cur_chunks = 0, cur_seg_len = 1, cur_nseg = 1;
   int stage = 0;
   // host streaming
@@ -886,7 +922,7 @@ int dalloc(T **p, size_t count) {
 void free_ctx(kbz_ctx *c) {
   if (!c) return;
   DevGuard g(c->device);
-  void *ptrs[] = {c->V[0], c->V[1], c->last, c->ignore, c->chunk_or, c->chunk_cls, c->flags,
+  void *ptrs[] = {c->V[0], c->V[1], c->last, c->ignore, c->chunk_or, c->chunk_cls, c->flags, c->fix_list,
                   c->skip, c->neq, c->h32, c->hnb32, c->segor, c->segprev, c->total,
                   c->items, c->counters, c->shard_last, c->dslot[0], c->dslot[1],
                   c->dslot_oc[0], c->dslot_oc[1], c->dres_hnb, c->dres_h32, c->dres_x64};
@@ -905,18 +941,13 @@ void free_ctx(kbz_ctx *c) {
 
 template <int MODE, bool IGN, bool X64>
 void launch_pass1(const Pass1Args &a, uint32_t chunks, hipStream_t s) {
-  static const int split = [] {
-    const char *e = getenv("KBZ_PASS1");
-    return e ? atoi(e) : 1;
-  }();
-  if (split) {
-    hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64>), dim3(chunks), dim3(128), 0, s, a);
-    return;
-  }
-  if (a.map_size % 512 == 0)
-    hipLaunchKernelGGL((k_pass1<MODE, IGN, X64, 512>), dim3(chunks), dim3(64), 0, s, a);
-  else
-    hipLaunchKernelGGL((k_pass1<MODE, IGN, X64, 256>), dim3(chunks), dim3(64), 0, s, a);
+#ifdef KBZ_ABLATION
+  static const int abl = getenv("KBZ_ABL") ? atoi(getenv("KBZ_ABL")) : 0;
+  if (abl == 1) { hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, 1>), dim3(chunks), dim3(128), 0, s, a); return; }
+  if (abl == 2) { hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, 2>), dim3(chunks), dim3(128), 0, s, a); return; }
+  if (abl == 3) { hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, 3>), dim3(chunks), dim3(128), 0, s, a); return; }
+#endif
+  hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64>), dim3(chunks), dim3(128), 0, s, a);
 }
 
 int pass1_dispatch(kbz_ctx *c, const Pass1Args &a, uint32_t chunks, bool x64, hipStream_t s) {
@@ -980,11 +1011,12 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   c->item_cap = (uint32_t)std::min<size_t>(kItemsPerCol * M * nc + 1024, 0xffffffffu);
   bool ok = !dalloc(&c->V[0], 3 * M) && !dalloc(&c->V[1], 3 * M) && !dalloc(&c->last, 2) &&
             !dalloc(&c->chunk_or, c->max_chunks * nc * M) && !dalloc(&c->chunk_cls, c->max_chunks) &&
-            !dalloc(&c->flags, c->max_chunks) && !dalloc(&c->skip, max_batch) &&
+            !dalloc(&c->flags, c->max_chunks) && !dalloc(&c->fix_list, c->max_chunks) &&
+            !dalloc(&c->skip, max_batch) &&
             !dalloc(&c->neq, max_batch) && !dalloc(&c->h32, max_batch) &&
             !dalloc(&c->hnb32, max_batch) && !dalloc(&c->segor, kMaxSeg * nc * M) &&
             !dalloc(&c->segprev, kMaxSeg * nc * M) && !dalloc(&c->total, nc * M) &&
-            !dalloc(&c->items, c->item_cap) && !dalloc(&c->counters, 4) &&
+            !dalloc(&c->items, c->item_cap) && !dalloc(&c->counters, 8) &&
             !dalloc(&c->shard_last, 2);
   if (!ok) {
     std::string e = g_err;
@@ -994,7 +1026,11 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   }
   (void)hipMemset(c->V[0], 0xff, 3 * M);
   (void)hipMemset(c->last, 0, 2 * sizeof(uint32_t));
-  (void)hipMemset(c->counters, 0, 4 * sizeof(uint32_t));
+  (void)hipMemset(c->counters, 0, 8 * sizeof(uint32_t));
+  // consumers re-zero these for the next batch (k_total: segor, k_pack: hnb32)
+  (void)hipMemset(c->segor, 0, kMaxSeg * nc * M);
+  (void)hipMemset(c->hnb32, 0, max_batch * sizeof(uint32_t));
+  (void)hipMemset(c->flags, 0, c->max_chunks * sizeof(uint32_t));
   if (hipDeviceSynchronize() != hipSuccess) {
     fail("device init failed");
     free_ctx(c);
@@ -1065,13 +1101,12 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
   c->cur_nseg = std::max(1u, std::min<unsigned>(kMaxSeg, c->cur_chunks));
   c->cur_seg_len = std::max(1u, cdiv(c->cur_chunks, c->cur_nseg));
   c->cur_nseg = std::max(1u, cdiv(c->cur_chunks, c->cur_seg_len));
+  HIP_TRY(hipMemsetAsync(c->counters, 0, 8 * sizeof(uint32_t), s));
   HIP_TRY(hipMemsetAsync(c->shard_last, 0, 2 * sizeof(uint32_t), s));
-  HIP_TRY(hipMemsetAsync(c->counters, 0, 4 * sizeof(uint32_t), s));
   if (n == 0) {
     c->stage = 1;
     return 0;
   }
-  HIP_TRY(hipMemsetAsync(c->hnb32, 0, n * sizeof(uint32_t), s));
   Pass1Args a;
   a.traces = traces;
   a.stride = stride;
@@ -1079,12 +1114,15 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
   a.map_size = (uint32_t)c->M;
   a.outcome = outcome;
   a.ignore = c->ignore;
-  a.h32 = c->h32;
+  a.h32 = h32_out ? h32_out : c->h32;  // hashes go straight to the caller's buffer
+  c->cur_h32 = a.h32;
   a.x64 = (want & KBZ_WANT_X64) ? x64_out : nullptr;
   a.neq = c->neq;
   a.chunk_or = c->chunk_or;
   a.chunk_cls = c->chunk_cls;
   a.shard_last = c->shard_last;
+  a.segor = c->segor;
+  a.seg_len = c->cur_seg_len;
   if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, s)) return -1;
   c->stage = 1;
   return 0;
@@ -1106,18 +1144,22 @@ int kbz_shard_link(kbz_ctx_t *c, const uint32_t *prev_last, int is_first,
   hipStream_t s = (hipStream_t)stream;
   if (c->mode == KBZ_MODE_DYNAMORIO) {
     const size_t n = c->cur_n;
-    if (n) HIP_TRY(hipMemsetAsync(c->flags, 0, c->cur_chunks, s));
     const int nl = c->lcur ^ 1;
-    hipLaunchKernelGGL(k_skip, dim3(std::max(1u, cdiv(n, 256))), dim3(256), 0, s, c->h32, c->neq,
-                       (uint32_t)n, is_first ? nullptr : prev_last, c->last + c->lcur,
+    hipLaunchKernelGGL(k_skip, dim3(std::max(1u, cdiv(n, 256))), dim3(256), 0, s, c->cur_h32,
+                       c->neq, (uint32_t)n, is_first ? nullptr : prev_last, c->last + c->lcur,
                        global_last ? global_last : c->shard_last, c->last + nl, c->skip,
-                       c->flags);
+                       c->flags, c->fix_list, c->counters + 3);
     HIP_TRY(hipGetLastError());
     c->lcur = nl;
     if (n) {
-      hipLaunchKernelGGL(k_fixchunk, dim3(cdiv(c->M / 16, 256), c->cur_chunks), dim3(256), 0, s,
-                         c->cur_traces, c->cur_stride, (uint32_t)n, (uint32_t)c->M, c->skip,
-                         c->flags, c->chunk_or);
+      // rarely-taken path: both kernels exit at once when the fix list is empty
+      hipLaunchKernelGGL(k_fixchunk, dim3(256), dim3(256), 0, s, c->cur_traces, c->cur_stride,
+                         (uint32_t)n, (uint32_t)c->M, c->skip, c->fix_list, c->counters + 3,
+                         c->chunk_or);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_segfix, dim3(256), dim3(256), 0, s, c->chunk_or, c->chunk_cls,
+                         c->cur_chunks, c->cur_seg_len, (uint32_t)c->M, c->fix_list,
+                         c->counters + 3, c->segor);
       HIP_TRY(hipGetLastError());
     }
   }
@@ -1129,17 +1171,12 @@ int kbz_shard_reduce(kbz_ctx_t *c, void *stream) {
   if (!c || c->stage != 2) return fail("kbz_shard_reduce: call kbz_shard_link first");
   DevGuard g(c->device);
   hipStream_t s = (hipStream_t)stream;
-  const unsigned gx = cdiv(c->M / 16, 256);
   if (c->cur_n == 0) {
     HIP_TRY(hipMemsetAsync(c->total, 0, c->nc * c->M, s));
-    HIP_TRY(hipMemsetAsync(c->segor, 0, c->nc * c->M, s));
+    HIP_TRY(hipMemsetAsync(c->segprev, 0, c->nc * c->M, s));
   } else {
-    hipLaunchKernelGGL(k_segor, dim3(gx, c->cur_nseg, c->nc), dim3(256), 0, s, c->chunk_or,
-                       c->chunk_cls, c->cur_chunks, c->cur_seg_len, c->nc, (uint32_t)c->M,
-                       c->segor);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_total, dim3(gx, 1, c->nc), dim3(256), 0, s, c->segor, c->cur_nseg,
-                       c->nc, (uint32_t)c->M, c->total);
+    hipLaunchKernelGGL(k_total, dim3(cdiv(c->M / 8, 256), 1, c->nc), dim3(256), 0, s, c->segor,
+                       c->cur_nseg, c->nc, (uint32_t)c->M, c->segprev, c->total);
     HIP_TRY(hipGetLastError());
   }
   c->stage = 3;
@@ -1166,31 +1203,25 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
   const int vn = c->vcur ^ 1;
   const uint8_t *ign = (c->mode == KBZ_MODE_DYNAMORIO) ? c->ignore : nullptr;
   const uint32_t nseg = c->cur_n ? c->cur_nseg : 1;
-  hipLaunchKernelGGL(k_prefix, dim3(gx, 1, c->nc), dim3(256), 0, s, c->segor, nseg, c->nc,
-                     (uint32_t)c->M, prefix, total, ign, c->V[c->vcur], c->V[vn], c->segprev);
+  hipLaunchKernelGGL(k_scan, dim3(gx, nseg, c->nc), dim3(256), 0, s, c->chunk_or, c->chunk_cls,
+                     c->cur_chunks, c->cur_seg_len, c->nc, (uint32_t)c->M, c->segprev, prefix,
+                     total, c->V[c->vcur], c->V[vn], ign, c->items, c->item_cap, c->counters);
   HIP_TRY(hipGetLastError());
   if (c->nc < 3)  // DYNAMORIO: tmout/crash maps are carried unchanged
     HIP_TRY(hipMemcpyAsync(c->V[vn] + c->nc * c->M, c->V[c->vcur] + c->nc * c->M,
                            (3 - c->nc) * c->M, hipMemcpyDeviceToDevice, s));
   if (c->cur_n) {
-    hipLaunchKernelGGL(k_scan, dim3(gx, c->cur_nseg, c->nc), dim3(256), 0, s, c->chunk_or,
-                       c->chunk_cls, c->cur_chunks, c->cur_seg_len, c->nc, (uint32_t)c->M,
-                       c->segprev, c->V[c->vcur], ign, c->items, c->item_cap, c->counters);
-    HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_resolve, dim3(512), dim3(256), 0, s, c->cur_traces, c->cur_stride,
                        (uint32_t)c->cur_n, c->mode, c->cur_outcome,
                        c->mode == KBZ_MODE_DYNAMORIO ? c->skip : nullptr, c->items, c->counters,
                        c->item_cap, c->hnb32, c->counters + 2);
     HIP_TRY(hipGetLastError());
-    if (hnb_out || c->cur_h32_out) {
-      if (hnb_out) {
-        hipLaunchKernelGGL(k_pack, dim3(cdiv(c->cur_n, 256)), dim3(256), 0, s, c->hnb32, c->h32,
-                           (uint32_t)c->cur_n, hnb_out, c->cur_h32_out);
-        HIP_TRY(hipGetLastError());
-      } else {
-        HIP_TRY(hipMemcpyAsync(c->cur_h32_out, c->h32, c->cur_n * 4, hipMemcpyDeviceToDevice, s));
-      }
-    }
+    hipLaunchKernelGGL(k_pack, dim3(cdiv(c->cur_n, 256)), dim3(256), 0, s, c->hnb32, c->cur_h32,
+                       (uint32_t)c->cur_n, hnb_out ? hnb_out : (uint8_t *)nullptr,
+                       (c->cur_h32_out && c->cur_h32_out != c->cur_h32) ? c->cur_h32_out : nullptr);
+    HIP_TRY(hipGetLastError());
+    if (c->mode == KBZ_MODE_DYNAMORIO)  // re-arm the fix-list flags of this batch
+      HIP_TRY(hipMemsetAsync(c->flags, 0, c->cur_chunks * sizeof(uint32_t), s));
   }
   c->vcur = vn;
   c->stage = 0;
@@ -1215,6 +1246,16 @@ int kbz_or_reduce(uint8_t *out, const uint8_t *in, size_t r_lo, size_t r_hi, siz
   HIP_TRY(hipGetLastError());
   return 0;
 }
+
+#ifdef KBZ_STAMPS
+// diagnostic build only: per (chunk, wave) cycles {compute, vmcnt wait, fill+prefetch, barrier}
+int kbz_debug_stamps(unsigned long long *host_out, size_t count) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_kbz_stamps),
+                              std::min<size_t>(count, 4096 * 2 * 4) * 8));
+  return 0;
+}
+#endif
 
 int kbz_sync(kbz_ctx_t *c, void *stream) {
   if (!c) return fail("null ctx");
