@@ -116,13 +116,17 @@ __device__ __forceinline__ void vmcnt_wait() {
 // Drain every asm load, keeping their destination registers live up to the wait: an asm
 // load's output looks ready to the compiler, so once it is dead the compiler may reuse the
 // register while the load is still in flight (the late write would clobber it).
-template <int NL>
-__device__ __forceinline__ void drain_asm_loads(const u32x4 (&r0)[NL], const u32x4 (&r1)[NL]) {
+template <int DD, int NL>
+__device__ __forceinline__ void drain_asm_loads(const u32x4 (&r)[DD][NL]) {
 #pragma unroll
-  for (int i = 0; i < NL; i++) asm volatile("" ::"v"(r0[i]), "v"(r1[i]));
+  for (int d = 0; d < DD; d++)
+#pragma unroll
+    for (int i = 0; i < NL; i++) asm volatile("" ::"v"(r[d][i]));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-  for (int i = 0; i < NL; i++) asm volatile("" ::"v"(r0[i]), "v"(r1[i]));
+  for (int d = 0; d < DD; d++)
+#pragma unroll
+    for (int i = 0; i < NL; i++) asm volatile("" ::"v"(r[d][i]));
 }
 // Diagnostic build only (-DKBZ_STAMPS): per-wave cycle accounting of pass 1's step phases,
 // read back by tools/stamps.py through kbz_debug_stamps().  No stamp executes otherwise.
@@ -186,24 +190,27 @@ struct Pass1Args {
 // ---------------------------------------------------------------------------------------------
 // pass 1: two waves per 64-trace chunk (lane = trace) sharing two 16-KiB LDS tile buffers.
 // Both waves stream: each loads half of every tile's rows (8 x 1-KiB coalesced wave-loads per
-// tile), two tiles ahead in registers.  A single loader wave per chunk cannot keep enough
-// loads in flight (tools/patprobe: ~4.5 TB/s vs ~6.6 TB/s with two).
+// tile) into a ring of D register buffers, D tiles ahead.  A single loader wave per chunk
+// cannot keep enough loads in flight (tools/patprobe: ~4.5 TB/s vs ~6.6 TB/s with two).
+// Measured on MI355X (profiles/r01_v5): D = 2, 3, 4, 6 all give 0.757-0.764 ms per 4 GiB
+// batch, so the default is D = 2 (KBZ_PASS1_DEPTH; fewest VGPRs).
 //   wave L: fills rows 0-31 of tile s+1, runs the serial per-trace chains (hash32 mix+step,
 //           optional XXH64) over tile s-1 after wave T transformed it;
 //   wave T: fills rows 32-63 of tile s, then per word transforms it in place (classify /
 //           simplify), ORs each column over the 64 traces (DPP), DynamoRIO equality with the
 //           previous trace; stores the chunk's column ORs and ORs them into the segment
 //           aggregate (64-bit atomics, nonzero words only).
-// Step s (one barrier per step): T fills+transforms tile s in buffer s&1 while L chains tile
-// s-1 and then refills that buffer with its half of tile s+1.  16-B slot q of row r lives at
-// slot q ^ (r & 15): fills (ds_write_b128, 4 rows per instruction) and the row-per-lane
-// ds_read_b128 are both bank-conflict-free.  Raw zero words stay 0 in LDS; a simplified
-// trace's transformed word is never 0, so L maps an untouched 0 of a simplified lane to
-// 0x0101010101010101.
+// Step s = 0..ntiles, rounded up to a multiple of D (no early exit from the unrolled ring:
+// every exit point would need its own copy of the ring registers), one barrier per step: T fills+transforms tile s in buffer s&1 while L
+// chains tile s-1 and then refills that buffer with its half of tile s+1.  16-B slot q of row r
+// lives at slot q ^ (r & 15): fills (ds_write_b128, 4 rows per instruction) and the
+// row-per-lane ds_read_b128 are both bank-conflict-free.  Raw zero words stay 0 in LDS; a
+// simplified trace's transformed word is never 0, so L maps an untouched 0 of a simplified
+// lane to 0x0101010101010101.
 // ABL (timing-only ablation builds, never used for results): 1 = T skips its per-word work,
 // 2 = L skips its chains, 3 = both.
 // ---------------------------------------------------------------------------------------------
-template <int MODE, bool IGN, bool X64, int ABL = 0>
+template <int MODE, bool IGN, bool X64, int ABL = 0, int D = 4>
 __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = 8;  // 8 x 1-KiB loads per wave per tile
@@ -222,7 +229,6 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   const int xf = valid ? class_xf(MODE, cls) : XF_RAW;
   const bool simp = (xf == XF_SIMPLIFY);
   const uint32_t ntiles = a.map_size / TW;
-  const uint32_t pairs = (ntiles + 1) / 2;
 
   // this wave's half of the rows: rows past the end of a partial chunk re-read its last row
   // (those lanes are invalid: masked out of the ORs, hashes not stored)
@@ -233,15 +239,15 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   for (int i = 0; i < NLD; i++)
     roff[i] = (uint32_t)(min(32 * wave + RPI * i + lr, nrows - 1) * a.stride);
   // Prefetch: asm loads, waited for by hand (vmcnt counts VMEM ops of this wave in issue
-  // order).  Wave L issues no other VMEM op in its loop: at each fill the only younger ops
-  // are the other buffer's 8 loads -> vmcnt(8).  Wave T prefetches before transforming and
-  // every transform issues >= 1 global store, so at each loop fill >= 9 younger ops exist
-  // -> vmcnt(9); its first fill (prologue) has exactly the other buffer's 8 -> vmcnt(8).
+  // order).  Every step issues exactly NLD loads (tiles past the end re-load the chunk's first 256 B), so
+  // when a buffer is consumed exactly D-1 younger load groups exist -> vmcnt((D-1)*NLD).
+  // Wave T's global stores are younger still: the count is a lower bound, which is safe.
+  // Branch-free: an if/else around the asm loads would merge their outputs with register
+  // copies the compiler believes are safe while the loads are still in flight.
   auto load_half = [&](u32x4 (&r)[NLD], uint32_t t) {
-    t = min(t, ntiles - 1);  // past the end: harmless re-read of the last tile
-    const uint8_t *p = lbase + (size_t)t * TW;
+    const uint32_t msk = t < ntiles ? ~0u : 0u;
 #pragma unroll
-    for (int i = 0; i < NLD; i++) asm_load16(r[i], p + roff[i]);
+    for (int i = 0; i < NLD; i++) asm_load16(r[i], lbase + ((t * TW + roff[i]) & msk));
   };
   auto store_half = [&](const u32x4 (&r)[NLD], int b) {
 #pragma unroll
@@ -251,7 +257,9 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
       lds[b * TILE + rr * SLOTS + (ls ^ (rr & 15))] = make_uint4(v.x, v.y, v.z, v.w);
     }
   };
-  u32x4 R0[NLD], R1[NLD];
+  u32x4 R[D][NLD];
+#pragma unroll
+  for (int d = 0; d < D; d++) load_half(R[d], d);
 
   if (wave == 0) {
     // ------------------------------------------------------------------ wave L
@@ -301,43 +309,31 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         v1 = n1;
       }
     };
-    // L's half of tile t is staged in R[t & 1].  Step s: chain tile s-1, store own half of
-    // tile s+1 into the buffer just chained, prefetch own half of tile s+3.  Loads/stores are
-    // unconditional (straight-line VMEM code keeps the compiler's counted vmcnt).
-    load_half(R0, 0);
-    load_half(R1, 1);
-    vmcnt_wait<NLD>();
-    store_half(R0, 0);
-    load_half(R0, 2);
-    lds_barrier();  // (A) L's half of tile 0 is in buffer 0
-    vmcnt_wait<NLD>();
-    store_half(R1, 1);  // step 0
-    load_half(R1, 3);
-    lds_barrier();
+    // prologue: own half of tile 0 -> buffer 0 (T transforms it at step 0)
+    vmcnt_wait<(D - 1) * NLD>();
+    store_half(R[0], 0);
+    load_half(R[0], D);
+    lds_barrier();  // (A)
     KBZ_STAMP_DECL;
-    for (uint32_t pi = 0; pi < pairs; pi++) {
-      const uint32_t s = 2 * pi + 1;
-      chain_tile(s - 1, 0);
-      KBZ_STAMP(0);
-      vmcnt_wait<NLD>();
-      KBZ_STAMP(1);
-      store_half(R0, 0);
-      load_half(R0, s + 3);
-      KBZ_STAMP(2);
-      lds_barrier();
-      KBZ_STAMP(3);
-      if (s < ntiles) chain_tile(s, 1);
-      KBZ_STAMP(0);
-      vmcnt_wait<NLD>();
-      KBZ_STAMP(1);
-      store_half(R1, 1);
-      load_half(R1, s + 4);
-      KBZ_STAMP(2);
-      lds_barrier();
-      KBZ_STAMP(3);
+    // step s: chain tile s-1, store own half of tile s+1 (ring slot (s+1)%D) into the buffer
+    // just chained, prefetch tile s+1+D into that slot.
+    for (uint32_t g = 0; g <= ntiles; g += D) {
+#pragma unroll
+      for (int u = 0; u < D; u++) {
+        const uint32_t s = g + u;
+        if (s >= 1 && s <= ntiles) chain_tile(s - 1, (s - 1) & 1);
+        KBZ_STAMP(0);
+        vmcnt_wait<(D - 1) * NLD>();
+        KBZ_STAMP(1);
+        store_half(R[(u + 1) % D], (s + 1) & 1);
+        load_half(R[(u + 1) % D], s + 1 + D);
+        KBZ_STAMP(2);
+        lds_barrier();
+        KBZ_STAMP(3);
+      }
     }
     KBZ_STAMP_FLUSH(chunk * 2 + 0);
-    drain_asm_loads(R0, R1);
+    drain_asm_loads(R);
     if (valid) {
       const uint32_t h32 = h32_final(h);
       a.h32[row0 + lane] = h32;
@@ -425,40 +421,27 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
           }
       }
     };
-    // T's half of tile t is staged in R[t & 1].  Step s: store own half of tile s (L's half
-    // arrived before the previous barrier), prefetch own half of tile s+2, transform tile s.
-    load_half(R0, 0);
-    load_half(R1, 1);
-    lds_barrier();  // (A)
-    vmcnt_wait<NLD>();
-    store_half(R0, 0);
-    load_half(R0, 2);
-    transform_tile(0);
-    lds_barrier();
+    lds_barrier();  // (A): L's half of tile 0 is in buffer 0
     KBZ_STAMP_DECL;
-    for (uint32_t pi = 0; pi < pairs; pi++) {
-      const uint32_t s = 2 * pi + 1;
-      vmcnt_wait<NLD + 1>();
-      KBZ_STAMP(1);
-      store_half(R1, 1);
-      load_half(R1, s + 2);
-      KBZ_STAMP(2);
-      if (s < ntiles) transform_tile(s);
-      KBZ_STAMP(0);
-      lds_barrier();
-      KBZ_STAMP(3);
-      vmcnt_wait<NLD + 1>();
-      KBZ_STAMP(1);
-      store_half(R0, 0);
-      load_half(R0, s + 3);
-      KBZ_STAMP(2);
-      if (s + 1 < ntiles) transform_tile(s + 1);
-      KBZ_STAMP(0);
-      lds_barrier();
-      KBZ_STAMP(3);
+    // step s: store own half of tile s (ring slot s%D), prefetch tile s+D into that slot,
+    // transform tile s.
+    for (uint32_t g = 0; g <= ntiles; g += D) {
+#pragma unroll
+      for (int u = 0; u < D; u++) {
+        const uint32_t s = g + u;
+        vmcnt_wait<(D - 1) * NLD>();
+        KBZ_STAMP(1);
+        store_half(R[u], s & 1);
+        load_half(R[u], s + D);
+        KBZ_STAMP(2);
+        if (s < ntiles) transform_tile(s);
+        KBZ_STAMP(0);
+        lds_barrier();
+        KBZ_STAMP(3);
+      }
     }
     KBZ_STAMP_FLUSH(chunk * 2 + 1);
-    drain_asm_loads(R0, R1);
+    drain_asm_loads(R);
     if (MODE == KBZ_MODE_DYNAMORIO && valid) a.neq[row0 + lane] = neq != 0;
   }
 }
@@ -939,15 +922,31 @@ void free_ctx(kbz_ctx *c) {
   delete c;
 }
 
+#ifndef KBZ_PASS1_DEPTH
+#define KBZ_PASS1_DEPTH 2
+#endif
+#ifdef KBZ_ABLATION
+template <int MODE, bool IGN, bool X64, int ABL>
+void launch_abl(int depth, const Pass1Args &a, uint32_t chunks, hipStream_t s) {
+  if (depth == 2) hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, ABL, 2>), dim3(chunks), dim3(128), 0, s, a);
+  else if (depth == 3) hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, ABL, 3>), dim3(chunks), dim3(128), 0, s, a);
+  else if (depth == 6) hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, ABL, 6>), dim3(chunks), dim3(128), 0, s, a);
+  else hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, ABL, 4>), dim3(chunks), dim3(128), 0, s, a);
+}
+#endif
 template <int MODE, bool IGN, bool X64>
 void launch_pass1(const Pass1Args &a, uint32_t chunks, hipStream_t s) {
 #ifdef KBZ_ABLATION
+  // timing-only builds: KBZ_ABL selects the ablation, KBZ_DEPTH the register ring depth
   static const int abl = getenv("KBZ_ABL") ? atoi(getenv("KBZ_ABL")) : 0;
-  if (abl == 1) { hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, 1>), dim3(chunks), dim3(128), 0, s, a); return; }
-  if (abl == 2) { hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, 2>), dim3(chunks), dim3(128), 0, s, a); return; }
-  if (abl == 3) { hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, 3>), dim3(chunks), dim3(128), 0, s, a); return; }
+  static const int depth = getenv("KBZ_DEPTH") ? atoi(getenv("KBZ_DEPTH")) : KBZ_PASS1_DEPTH;
+  if (abl == 1) return launch_abl<MODE, IGN, X64, 1>(depth, a, chunks, s);
+  if (abl == 2) return launch_abl<MODE, IGN, X64, 2>(depth, a, chunks, s);
+  if (abl == 3) return launch_abl<MODE, IGN, X64, 3>(depth, a, chunks, s);
+  return launch_abl<MODE, IGN, X64, 0>(depth, a, chunks, s);
+#else
+  hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, 0, KBZ_PASS1_DEPTH>), dim3(chunks), dim3(128), 0, s, a);
 #endif
-  hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64>), dim3(chunks), dim3(128), 0, s, a);
 }
 
 int pass1_dispatch(kbz_ctx *c, const Pass1Args &a, uint32_t chunks, bool x64, hipStream_t s) {

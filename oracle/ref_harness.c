@@ -6,7 +6,7 @@
  * committed golden fixtures can be pinned against it.  Built by oracle/Makefile into
  * oracle/_ref/libkbz_ref.so; nothing of the reference is copied into the repository: the
  * function bodies are pulled in at build time with #include / sed-extracted .inc files that
- * live only in oracle/_ref/ (git-ignored).
+ * live only in a temporary build directory outside the repository (oracle/Makefile TMP).
  *
  * One translation unit per (source, MAP_SIZE) pair, selected with -D flags by the Makefile:
  *   REF_AFL   instrumentation/afl_instrumentation.c:116-121 (merge_bitmaps),

@@ -7,12 +7,12 @@ export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
 STEPS="${STEPS:-tests bench prof}"
-PYTEST_ARGS="${PYTEST_ARGS:--m gpu -x -q}"
+PYTEST_ARGS="${PYTEST_ARGS:--m gpu -x -v --timeout 120 --timeout-method thread}"
 for s in $STEPS; do
   case $s in
     tests)
       echo "== pytest $PYTEST_ARGS $(date +%T)"
-      timeout -k 10 ${TEST_TIMEOUT:-900} python -m pytest tests $PYTEST_ARGS > $OUT/pytest_gpu.log 2>&1
+      timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests $PYTEST_ARGS > $OUT/pytest_gpu.log 2>&1
       rc=$?; tail -25 $OUT/pytest_gpu.log; echo "pytest rc=$rc"
       [ $rc -le 1 ] || exit $rc ;;
     smoke)

@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of pass 1 from rocprofv3 PMC passes (scripts/gpu_session.sh pmc).
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  gfx950 correction (MI355X_MICROARCH.md,
+HBM section): FETCH_SIZE counts wide coalesced 16-B/lane streaming reads at half their bytes
+(128-B requests tallied as 64 B), so it is doubled; WRITE_SIZE is exact for such stores.
+Writes profiles/<tag>/pass1_traffic.json and profiles/pass1_traffic.json (read by bench.py).
+
+usage: pmc_traffic.py <gpurun_out dir> <tag>
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = "k_pass1s"
+
+
+def per_dispatch(pattern, counter):
+    vals = []
+    for f in glob.glob(pattern, recursive=True):
+        for r in csv.DictReader(open(f)):
+            if KERNEL in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
+                vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    out, tag = sys.argv[1], sys.argv[2]
+    fetch = per_dispatch(os.path.join(out, "pmc1", "**", "*counter_collection.csv"), "FETCH_SIZE")
+    write = per_dispatch(os.path.join(out, "pmc2", "**", "*counter_collection.csv"), "WRITE_SIZE")
+    if not fetch:
+        sys.exit("no FETCH_SIZE rows for " + KERNEL)
+    f_kib = sorted(fetch)[len(fetch) // 2]
+    w_kib = sorted(write)[len(write) // 2] if write else 0.0
+    read_bytes = 2.0 * f_kib * 1024.0
+    write_bytes = w_kib * 1024.0
+    res = {"kernel": KERNEL, "dispatches": len(fetch),
+           "fetch_size_kib_raw_median": f_kib, "write_size_kib_median": w_kib,
+           "hbm_read_bytes_per_launch": read_bytes, "hbm_write_bytes_per_launch": write_bytes,
+           "hbm_bytes_per_launch": read_bytes + write_bytes,
+           "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), WRITE_SIZE as is"}
+    os.makedirs(os.path.join(ROOT, "profiles", tag), exist_ok=True)
+    for p in (os.path.join(ROOT, "profiles", tag, "pass1_traffic.json"),
+              os.path.join(ROOT, "profiles", "pass1_traffic.json")):
+        json.dump(res, open(p, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
