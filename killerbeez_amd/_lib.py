@@ -61,7 +61,8 @@ def lib(build_if_missing: bool = True):
     global _LIB
     if _LIB is not None:
         return _LIB
-    path = _build.HIP_LIB
+    # KBZ_HIP_LIB: load an alternative in-tree build (A/B timing of kernel variants)
+    path = os.environ.get("KBZ_HIP_LIB") or _build.HIP_LIB
     if not os.path.exists(path):
         if not build_if_missing:
             raise KbzError(f"{path} not built (run killerbeez_amd.build.build_all())")
