@@ -1,0 +1,539 @@
+/*
+ * killerbeez_amd/csrc/kbz_plugin.c -- libkbz_plugin.so: the "afl_gpu" and "dynamorio_gpu"
+ * instrumentation plugins of include/kbz_plugin.h.
+ *
+ * Every novelty result and every merge comes from libkbz_hip.so on the GPU; this file is the
+ * host bookkeeping around it: options/state JSON, a host mirror of the virgin maps (so
+ * get_state/set_state/merge work without replaying anything), the deferred per-exec queue that
+ * turns the reference's one-exec-at-a-time calls into ordered GPU batches, and the vtable.
+ * There is no CPU path: if the HIP library cannot reach a GPU, triage and merge calls fail
+ * with the reference's error values.
+ *
+ * Reference behaviour mirrored (paths relative to ThePatrickStar/killerbeez):
+ *   create/set_state      afl_create :23-35, afl_set_state :95-109 (3 maps), dynamorio_set_state
+ *                         :1311-1372 (virgin_bits + last_shm_hash); fresh maps are all-0xff
+ *                         (setup_shm afl_instrumentation.c:555-559)
+ *   get_state             afl_get_state :62-79, dynamorio_get_state :1239-1281 (key names)
+ *   merge                 afl_merge :123-140 (AND of the 3 maps, everything else fresh),
+ *                         dynamorio_merge :1180-1231 (AND of virgin_bits, last hash 0)
+ *   is_new_path           afl_is_new_path :189-198 (last_is_new_path ? 1 : 0; -1 before the
+ *                         first exec), dynamorio has_new_coverage :1465-1467 (hnb != 0)
+ *   get_fuzz_result       afl_get_fuzz_result :208-216 (the recorded FUZZ_* of the last exec)
+ *   ignore_bytes_file     load_ignore_bytes dynamorio_instrumentation.c:788-801 (exactly
+ *                         map_size bytes)
+ */
+#define _POSIX_C_SOURCE 200809L /* strdup under -std=c11 */
+#include "kbz_plugin.h"
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "kbz_triage.h"
+
+static __thread char g_err[512];
+
+static void set_err(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+const char *kbz_plugin_last_error(void) { return g_err; }
+
+typedef struct kbz_plugin {
+  int mode;                /* KBZ_MODE_AFL or KBZ_MODE_DYNAMORIO */
+  size_t map_size, max_batch;
+  uint8_t *ignore;         /* dynamorio_gpu ignore_bytes (map_size bytes) or NULL */
+  uint8_t *virgin;         /* host mirror: virgin_bits | virgin_tmout | virgin_crash */
+  uint32_t last_hash;      /* dynamorio last_shm_hash */
+  int mirror_stale;        /* the GPU copy is newer than the mirror */
+  kbz_ctx_t *ctx;          /* GPU context, created on the first triage */
+  uint8_t *q_traces;       /* deferred execs, max_batch rows */
+  int8_t *q_outcome;
+  size_t q_n;
+  long q_base;             /* ticket of q_traces[0] */
+  uint8_t *r_hnb;          /* results of the last flushed window */
+  size_t r_n;
+  long r_base;
+  long last_ticket;        /* -1 until the first record */
+  int last_fuzz_result;
+} kbz_plugin_t;
+
+static size_t nmaps(const kbz_plugin_t *p) { return p->mode == KBZ_MODE_DYNAMORIO ? 1 : 3; }
+
+/* ---- minimal JSON: flat objects with number / string values (the formats of this file) ---- */
+static const char *json_value(const char *json, const char *key) {
+  char pat[96];
+  snprintf(pat, sizeof(pat), "\"%s\"", key);
+  for (const char *p = json; (p = strstr(p, pat)); p++) {
+    const char *q = p + strlen(pat);
+    while (*q == ' ' || *q == '\t' || *q == '\n' || *q == '\r') q++;
+    if (*q != ':') continue;
+    q++;
+    while (*q == ' ' || *q == '\t' || *q == '\n' || *q == '\r') q++;
+    return q;
+  }
+  return NULL;
+}
+
+/* 1 found, 0 absent, -1 malformed */
+static int json_u64(const char *json, const char *key, unsigned long long *out) {
+  const char *v = json ? json_value(json, key) : NULL;
+  if (!v) return 0;
+  char *end;
+  unsigned long long x = strtoull(v, &end, 10);
+  if (end == v) return -1;
+  *out = x;
+  return 1;
+}
+
+static char *json_str(const char *json, const char *key) {
+  const char *v = json ? json_value(json, key) : NULL;
+  if (!v || *v != '"') return NULL;
+  v++;
+  char *s = (char *)malloc(strlen(v) + 1);
+  if (!s) return NULL;
+  size_t n = 0;
+  for (; *v && *v != '"'; v++) {
+    if (*v == '\\' && v[1]) v++;
+    s[n++] = *v;
+  }
+  s[n] = 0;
+  return s;
+}
+
+static int hexval(char c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  return -1;
+}
+
+static int json_hex(const char *json, const char *key, uint8_t *out, size_t n) {
+  const char *v = json_value(json, key);
+  if (!v || *v != '"') return -1;
+  v++;
+  for (size_t i = 0; i < n; i++) {
+    const int hi = hexval(v[2 * i]);
+    const int lo = hi < 0 ? -1 : hexval(v[2 * i + 1]);
+    if (hi < 0 || lo < 0) return -1;
+    out[i] = (uint8_t)(hi << 4 | lo);
+  }
+  return v[2 * n] == '"' ? 0 : -1;
+}
+
+static char *put_hex(char *o, const uint8_t *b, size_t n) {
+  static const char digits[] = "0123456789abcdef";
+  for (size_t i = 0; i < n; i++) {
+    *o++ = digits[b[i] >> 4];
+    *o++ = digits[b[i] & 15];
+  }
+  return o;
+}
+
+/* ---- lifetime ------------------------------------------------------------------------------ */
+static void plugin_free(kbz_plugin_t *p) {
+  if (!p) return;
+  if (p->ctx) kbz_ctx_destroy(p->ctx);
+  free(p->ignore);
+  free(p->virgin);
+  free(p->q_traces);
+  free(p->q_outcome);
+  free(p->r_hnb);
+  free(p);
+}
+
+static kbz_plugin_t *plugin_alloc(int mode, size_t map_size, size_t max_batch) {
+  kbz_plugin_t *p = (kbz_plugin_t *)calloc(1, sizeof(*p));
+  if (!p) return NULL;
+  p->mode = mode;
+  p->map_size = map_size;
+  p->max_batch = max_batch;
+  p->last_ticket = -1;
+  p->last_fuzz_result = KBZ_PLUGIN_FUZZ_ERROR;
+  p->virgin = (uint8_t *)malloc(3 * map_size);
+  p->q_traces = (uint8_t *)malloc(max_batch * map_size);
+  p->q_outcome = (int8_t *)malloc(max_batch);
+  p->r_hnb = (uint8_t *)malloc(max_batch);
+  if (!p->virgin || !p->q_traces || !p->q_outcome || !p->r_hnb) {
+    plugin_free(p);
+    set_err("out of host memory");
+    return NULL;
+  }
+  memset(p->virgin, 0xff, 3 * map_size);
+  return p;
+}
+
+static int load_ignore(kbz_plugin_t *p, const char *path) {
+  FILE *f = fopen(path, "rb");
+  if (!f) {
+    set_err("Could not open ignore bytes file %s", path);
+    return -1;
+  }
+  p->ignore = (uint8_t *)malloc(p->map_size);
+  size_t got = p->ignore ? fread(p->ignore, 1, p->map_size, f) : 0;
+  const int extra = fgetc(f) != EOF;
+  fclose(f);
+  if (got != p->map_size || extra) {
+    set_err("Incorrect size of ignore bytes file %s (need exactly %zu bytes)", path, p->map_size);
+    return -1;
+  }
+  return 0;
+}
+
+static kbz_plugin_t *plugin_from_options(int mode, const char *options) {
+  unsigned long long m = 65536, mb = 4096;
+  if (json_u64(options, "map_size", &m) < 0 || json_u64(options, "max_batch", &mb) < 0) {
+    set_err("bad options (map_size / max_batch must be integers)");
+    return NULL;
+  }
+  if (m < 256 || m % 256 || m > (1ull << 24)) {
+    set_err("map_size must be a multiple of 256 in [256, 16 MiB]");
+    return NULL;
+  }
+  if (mb < 1 || mb * m > (1ull << 34)) {
+    set_err("max_batch must be >= 1 and max_batch * map_size <= 16 GiB");
+    return NULL;
+  }
+  kbz_plugin_t *p = plugin_alloc(mode, (size_t)m, (size_t)mb);
+  if (!p) return NULL;
+  char *ign = mode == KBZ_MODE_DYNAMORIO ? json_str(options, "ignore_bytes_file") : NULL;
+  if (ign) {
+    const int rc = load_ignore(p, ign);
+    free(ign);
+    if (rc) {
+      plugin_free(p);
+      return NULL;
+    }
+  }
+  return p;
+}
+
+/* a fresh state with the same configuration (merge results) */
+static kbz_plugin_t *plugin_clone_config(const kbz_plugin_t *src) {
+  kbz_plugin_t *p = plugin_alloc(src->mode, src->map_size, src->max_batch);
+  if (p && src->ignore) {
+    p->ignore = (uint8_t *)malloc(src->map_size);
+    if (!p->ignore) {
+      plugin_free(p);
+      set_err("out of host memory");
+      return NULL;
+    }
+    memcpy(p->ignore, src->ignore, src->map_size);
+  }
+  return p;
+}
+
+/* ---- GPU side ------------------------------------------------------------------------------ */
+static int ensure_ctx(kbz_plugin_t *p) {
+  if (p->ctx) return 0;
+  p->ctx = kbz_ctx_create(p->map_size, p->mode, p->max_batch);
+  if (!p->ctx) {
+    set_err("GPU context: %s", kbz_last_error());
+    return -1;
+  }
+  if (kbz_set_virgin(p->ctx, p->virgin) || kbz_set_last_hash(p->ctx, p->last_hash) ||
+      (p->ignore && kbz_set_ignore(p->ctx, p->ignore))) {
+    set_err("GPU state upload: %s", kbz_last_error());
+    kbz_ctx_destroy(p->ctx);
+    p->ctx = NULL;
+    return -1;
+  }
+  return 0;
+}
+
+static int sync_mirror(kbz_plugin_t *p) {
+  if (!p->ctx || !p->mirror_stale) return 0;
+  if (kbz_get_virgin(p->ctx, p->virgin) || kbz_get_last_hash(p->ctx, &p->last_hash)) {
+    set_err("GPU state download: %s", kbz_last_error());
+    return -1;
+  }
+  p->mirror_stale = 0;
+  return 0;
+}
+
+static int plugin_flush(kbz_plugin_t *p) {
+  if (!p->q_n) return 0;
+  if (ensure_ctx(p)) return -1;
+  p->mirror_stale = 1;
+  if (kbz_triage_batch_host(p->ctx, p->q_traces, p->q_n, p->map_size, p->q_outcome, p->r_hnb,
+                            NULL, NULL, 0)) {
+    set_err("GPU triage: %s", kbz_last_error());
+    return -1;
+  }
+  p->r_base = p->q_base;
+  p->r_n = p->q_n;
+  p->q_base += (long)p->q_n;
+  p->q_n = 0;
+  return 0;
+}
+
+static long plugin_record(kbz_plugin_t *p, const uint8_t *trace, int fuzz_result) {
+  if (!p || !trace) {
+    set_err("null argument");
+    return -1;
+  }
+  if (fuzz_result != KBZ_PLUGIN_FUZZ_NONE && fuzz_result != KBZ_PLUGIN_FUZZ_HANG &&
+      fuzz_result != KBZ_PLUGIN_FUZZ_CRASH) {
+    set_err("fuzz_result must be FUZZ_NONE, FUZZ_HANG or FUZZ_CRASH");
+    return -1;
+  }
+  if (p->q_n == p->max_batch && plugin_flush(p)) return -1;
+  memcpy(p->q_traces + p->q_n * p->map_size, trace, p->map_size);
+  /* the KBZ_FUZZ_* outcomes of kbz_triage.h use the same numbering */
+  p->q_outcome[p->q_n] = (int8_t)fuzz_result;
+  p->last_ticket = p->q_base + (long)p->q_n++;
+  p->last_fuzz_result = fuzz_result;
+  return p->last_ticket;
+}
+
+static int plugin_result(kbz_plugin_t *p, long ticket) {
+  if (!p || ticket < 0) {
+    set_err("no exec recorded");
+    return -1;
+  }
+  if (ticket >= p->q_base && plugin_flush(p)) return -1;
+  if (ticket < p->r_base || ticket >= p->r_base + (long)p->r_n) {
+    set_err("exec %ld is outside the last triaged window [%ld, %ld)", ticket, p->r_base,
+            p->r_base + (long)p->r_n);
+    return -1;
+  }
+  return p->r_hnb[ticket - p->r_base];
+}
+
+static int plugin_triage_batch(kbz_plugin_t *p, const uint8_t *traces, size_t n, size_t stride,
+                               const int8_t *outcome, uint8_t *hnb, uint32_t *h32,
+                               uint64_t *x64) {
+  if (!p || (n && !traces) || stride < p->map_size) {
+    set_err("bad arguments (null traces or stride < map_size)");
+    return -1;
+  }
+  if (plugin_flush(p) || ensure_ctx(p)) return -1; /* queued execs come first */
+  const int want = (h32 ? KBZ_WANT_H32 : 0) | (x64 ? KBZ_WANT_X64 : 0);
+  p->mirror_stale = 1;
+  for (size_t lo = 0; lo < n; lo += p->max_batch) {
+    const size_t cnt = n - lo < p->max_batch ? n - lo : p->max_batch;
+    if (kbz_triage_batch_host(p->ctx, traces + lo * stride, cnt, stride,
+                              outcome ? outcome + lo : NULL, hnb ? hnb + lo : NULL,
+                              h32 ? h32 + lo : NULL, x64 ? x64 + lo : NULL, want)) {
+      set_err("GPU triage: %s", kbz_last_error());
+      return -1;
+    }
+  }
+  return 0;
+}
+
+/* ---- state --------------------------------------------------------------------------------- */
+static const char *const kMapNames[3] = {"virgin_bits", "virgin_tmout", "virgin_crash"};
+
+static char *plugin_get_state(kbz_plugin_t *p) {
+  if (!p) {
+    set_err("null state");
+    return NULL;
+  }
+  if (plugin_flush(p) || sync_mirror(p)) return NULL;
+  const size_t m = p->map_size, k = nmaps(p);
+  char *s = (char *)malloc(256 + k * (2 * m + 32));
+  if (!s) {
+    set_err("out of host memory");
+    return NULL;
+  }
+  char *o = s + sprintf(s, "{\"map_size\":%zu", m);
+  for (size_t i = 0; i < k; i++) {
+    o += sprintf(o, ",\"%s\":\"", kMapNames[i]);
+    o = put_hex(o, p->virgin + i * m, m);
+    *o++ = '"';
+  }
+  if (p->mode == KBZ_MODE_DYNAMORIO) o += sprintf(o, ",\"last_shm_hash\":%u", p->last_hash);
+  *o++ = '}';
+  *o = 0;
+  return s;
+}
+
+static int plugin_set_state(kbz_plugin_t *p, const char *json) {
+  if (!p || !json) {
+    set_err("null argument");
+    return 1;
+  }
+  unsigned long long m = 0, h = 0;
+  if (json_u64(json, "map_size", &m) == 1 && m != p->map_size) {
+    set_err("state map_size %llu does not match the plugin's %zu", m, p->map_size);
+    return 1;
+  }
+  /* execs recorded before the new state was loaded belong to the old one */
+  if (plugin_flush(p)) return 1;
+  const size_t ms = p->map_size, k = nmaps(p);
+  uint8_t *v = (uint8_t *)malloc(3 * ms);
+  if (!v) {
+    set_err("out of host memory");
+    return 1;
+  }
+  memset(v, 0xff, 3 * ms);
+  for (size_t i = 0; i < k; i++) {
+    if (json_hex(json, kMapNames[i], v + i * ms, ms)) {
+      set_err("state lacks a valid \"%s\" (%zu bytes as hex)", kMapNames[i], ms);
+      free(v);
+      return 1;
+    }
+  }
+  if (p->mode == KBZ_MODE_DYNAMORIO && json_u64(json, "last_shm_hash", &h) < 0) {
+    set_err("bad last_shm_hash");
+    free(v);
+    return 1;
+  }
+  if (p->ctx && (kbz_set_virgin(p->ctx, v) || kbz_set_last_hash(p->ctx, (uint32_t)h))) {
+    set_err("GPU state upload: %s", kbz_last_error());
+    free(v);
+    return 1;
+  }
+  memcpy(p->virgin, v, 3 * ms);
+  free(v);
+  p->last_hash = (uint32_t)h;
+  p->mirror_stale = 0;
+  return 0;
+}
+
+static kbz_plugin_t *plugin_create(int mode, const char *options, const char *state) {
+  kbz_plugin_t *p = plugin_from_options(mode, options);
+  if (p && state && plugin_set_state(p, state)) {
+    plugin_free(p);
+    return NULL;
+  }
+  return p;
+}
+
+/* ---- merge --------------------------------------------------------------------------------- */
+static kbz_plugin_t *plugin_merge_many(kbz_plugin_t **ps, size_t n) {
+  if (!ps || !n || !ps[0]) {
+    set_err("nothing to merge");
+    return NULL;
+  }
+  for (size_t i = 0; i < n; i++) {
+    if (!ps[i] || ps[i]->mode != ps[0]->mode || ps[i]->map_size != ps[0]->map_size) {
+      set_err("states to merge must come from the same plugin with the same map_size");
+      return NULL;
+    }
+    if (plugin_flush(ps[i]) || sync_mirror(ps[i])) return NULL;
+  }
+  const size_t row = nmaps(ps[0]) * ps[0]->map_size;
+  uint8_t *rows = (uint8_t *)malloc(n * row);
+  kbz_plugin_t *r = rows ? plugin_clone_config(ps[0]) : NULL;
+  if (!r) {
+    free(rows);
+    if (!rows) set_err("out of host memory");
+    return NULL;
+  }
+  for (size_t i = 0; i < n; i++) memcpy(rows + i * row, ps[i]->virgin, row);
+  const int rc = kbz_merge_and_host(r->virgin, rows, n, row);
+  free(rows);
+  if (rc) {
+    set_err("GPU merge: %s", kbz_last_error());
+    plugin_free(r);
+    return NULL;
+  }
+  r->last_hash = 0; /* dynamorio_merge :1228; afl_merge starts everything but the maps fresh */
+  return r;
+}
+
+static const char kHelpAfl[] =
+    "afl_gpu - AFL bitmap triage (has_new_bits vs virgin_bits/tmout/crash) on the GPU\n"
+    "Options:\n"
+    "  map_size              Trace map size in bytes (default 65536)\n"
+    "  max_batch             Execs triaged per GPU batch (default 4096)\n";
+static const char kHelpDr[] =
+    "dynamorio_gpu - DynamoRIO/winafl triage (classify_counts, hash32, last-hash skip,\n"
+    "                has_new_bits) on the GPU\n"
+    "Options:\n"
+    "  map_size              Trace map size in bytes (default 65536)\n"
+    "  max_batch             Execs triaged per GPU batch (default 4096)\n"
+    "  ignore_bytes_file     File of map_size bytes: nonzero bytes are ignored\n";
+
+static int plugin_help(int mode, char **help_str) {
+  if (!help_str) return -1;
+  *help_str = strdup(mode == KBZ_MODE_DYNAMORIO ? kHelpDr : kHelpAfl);
+  return *help_str ? 0 : -1;
+}
+
+/* ---- exported entry points ------------------------------------------------------------------ */
+#define KBZ_PLUGIN_ENTRY_POINTS(P, MODE, NAME)                                                   \
+  void *P##_create(char *options, char *state) { return plugin_create(MODE, options, state); } \
+  void P##_cleanup(void *s) { plugin_free((kbz_plugin_t *)s); }                                \
+  void *P##_merge(void *a, void *b) {                                                          \
+    kbz_plugin_t *v[2] = {(kbz_plugin_t *)a, (kbz_plugin_t *)b};                               \
+    return (a && b) ? plugin_merge_many(v, 2) : (set_err("null state"), (void *)NULL);         \
+  }                                                                                            \
+  void *P##_merge_many(void **s, size_t n) { return plugin_merge_many((kbz_plugin_t **)s, n); } \
+  char *P##_get_state(void *s) { return plugin_get_state((kbz_plugin_t *)s); }                 \
+  void P##_free_state(char *s) { free(s); }                                                    \
+  int P##_set_state(void *s, char *json) { return plugin_set_state((kbz_plugin_t *)s, json); } \
+  int P##_enable(void *s, pid_t *process, char *cmd_line, char *input, size_t input_length) {  \
+    (void)s, (void)process, (void)cmd_line, (void)input, (void)input_length;                   \
+    set_err(NAME ": process control stays with the host instrumentation; hand each exec's "    \
+                 "trace to " #P "_record (INTEGRATION.md)");                                   \
+    return -1;                                                                                 \
+  }                                                                                            \
+  int P##_is_process_done(void *s) {                                                           \
+    (void)s;                                                                                   \
+    set_err(NAME ": no target process is run by this plugin");                                 \
+    return -1;                                                                                 \
+  }                                                                                            \
+  int P##_get_fuzz_result(void *s) {                                                           \
+    kbz_plugin_t *p = (kbz_plugin_t *)s;                                                       \
+    return (p && p->last_ticket >= 0) ? p->last_fuzz_result : KBZ_PLUGIN_FUZZ_ERROR;           \
+  }                                                                                            \
+  int P##_is_new_path(void *s) {                                                               \
+    kbz_plugin_t *p = (kbz_plugin_t *)s;                                                       \
+    const int r = p ? plugin_result(p, p->last_ticket) : -1;                                   \
+    return r < 0 ? -1 : (r ? 1 : 0);                                                           \
+  }                                                                                            \
+  int P##_triage_batch(void *s, const uint8_t *t, size_t n, size_t stride, const int8_t *oc,   \
+                       uint8_t *hnb, uint32_t *h32, uint64_t *x64) {                           \
+    return plugin_triage_batch((kbz_plugin_t *)s, t, n, stride, oc, hnb, h32, x64);            \
+  }                                                                                            \
+  int P##_help(char **help_str) { return plugin_help(MODE, help_str); }                        \
+  long P##_record(void *s, const uint8_t *t, int fuzz_result) {                                \
+    return plugin_record((kbz_plugin_t *)s, t, fuzz_result);                                   \
+  }                                                                                            \
+  int P##_result(void *s, long ticket) { return plugin_result((kbz_plugin_t *)s, ticket); }    \
+  int P##_flush(void *s) { return s ? plugin_flush((kbz_plugin_t *)s) : -1; }
+
+KBZ_PLUGIN_ENTRY_POINTS(kbz_afl_gpu, KBZ_MODE_AFL, "afl_gpu")
+KBZ_PLUGIN_ENTRY_POINTS(kbz_dynamorio_gpu, KBZ_MODE_DYNAMORIO, "dynamorio_gpu")
+
+#define KBZ_FILL_VTABLE(r, P)          \
+  do {                                 \
+    (r)->create = P##_create;          \
+    (r)->cleanup = P##_cleanup;        \
+    (r)->merge = P##_merge;            \
+    (r)->get_state = P##_get_state;    \
+    (r)->free_state = P##_free_state;  \
+    (r)->set_state = P##_set_state;    \
+    (r)->enable = P##_enable;          \
+    (r)->is_new_path = P##_is_new_path; \
+    (r)->get_fuzz_result = P##_get_fuzz_result; \
+    (r)->is_process_done = P##_is_process_done; \
+    (r)->triage_batch = P##_triage_batch; \
+    (r)->merge_many = P##_merge_many;  \
+  } while (0)
+
+kbz_instrumentation_t *kbz_instrumentation_factory(const char *name) {
+  if (!name) {
+    set_err("null instrumentation name");
+    return NULL;
+  }
+  kbz_instrumentation_t *r = (kbz_instrumentation_t *)calloc(1, sizeof(*r));
+  if (!r) return NULL;
+  if (!strcmp(name, "afl_gpu")) {
+    KBZ_FILL_VTABLE(r, kbz_afl_gpu);
+  } else if (!strcmp(name, "dynamorio_gpu")) {
+    KBZ_FILL_VTABLE(r, kbz_dynamorio_gpu);
+  } else {
+    free(r);
+    set_err("unknown instrumentation %s", name);
+    return NULL;
+  }
+  return r;
+}

@@ -1,0 +1,45 @@
+"""Static check of pass 1's hand-counted VMEM waits (tools/vmem_hazard_cfg.py).
+
+k_pass1s issues its prefetch loads from inline asm, which the compiler does not track: it
+may copy, reuse or overwrite a destination register before the hand-written
+`s_waitcnt vmcnt(N)`.  This compiles the device code to ISA, walks every k_pass1s
+instantiation as a control-flow graph with an in-order vmcnt queue, and requires that no
+instruction touches a register whose load may still be in flight.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+@pytest.mark.parametrize("flags", [[], ["-DKBZ_ABLATION"]], ids=["product", "ablation"])
+def test_pass1_has_no_inflight_register_hazards(tmp_path, flags):
+    import vmem_hazard_cfg as V
+    from killerbeez_amd import build
+
+    out = tmp_path / "k.s"
+    subprocess.check_call([build.hipcc(), f"--offload-arch={build.ARCH}", "-O3", "-std=c++17",
+                           "--cuda-device-only", "-S", "-I", build.INC, "-I", build.CSRC,
+                           *flags, build.HIP_SOURCES[0], "-o", str(out)],
+                          stderr=subprocess.DEVNULL)
+    funcs = V.split_functions(out.read_text().split("\n"))
+    pass1 = {k: v for k, v in funcs.items() if "k_pass1s" in k}
+    assert pass1, "no k_pass1s instantiation found in the ISA"
+    bad = {k: V.scan_function(v) for k, v in pass1.items()}
+    bad = {k: v[:3] for k, v in bad.items() if v}
+    assert not bad, bad
+
+
+def test_checker_catches_a_reused_destination():
+    """A register reused while its asm load is in flight must be reported."""
+    import vmem_hazard_cfg as V
+
+    body = ["global_load_dwordx4 v[2:5], v[0:1], off nt",
+            "v_mov_b32_e32 v3, 0",
+            "s_waitcnt vmcnt(0)",
+            "s_endpgm"]
+    assert V.scan_function(body)

@@ -1,0 +1,190 @@
+"""The instrumentation_t-layout plugins of libkbz_plugin.so (include/kbz_plugin.h).
+
+CPU part: the factory fills the reference's vtable order (instrumentation/instrumentation.h:
+40-62) plus the appended members, options/state JSON round-trips without touching a GPU, and
+every call that needs the GPU fails loudly instead of falling back to a CPU path.
+
+GPU part (-m gpu): the plugins driven the way fuzzer/main.c:370-418 drives a plugin (one exec
+at a time, is_new_path after each) and in deferred/batched form, bit-exact against the oracle's
+sequential per-exec loop; state dump/load and the merger fold against the oracle.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from killerbeez_amd import plugin as P
+from killerbeez_amd import synth
+
+M = 4096
+
+
+def _fn_addr(name):
+    return C.cast(getattr(P.lib(), name), C.c_void_p).value
+
+
+# ---- CPU ----------------------------------------------------------------------------------------
+
+def test_factory_vtable_order():
+    L = P.lib()
+    assert C.sizeof(P.VTable) == 14 * 8
+    for name in P.PLUGINS:
+        vt = L.kbz_instrumentation_factory(name.encode())
+        assert vt
+        v = vt.contents
+        for member in ("create", "cleanup", "merge", "get_state", "free_state", "set_state",
+                       "enable", "is_new_path", "get_fuzz_result", "is_process_done",
+                       "triage_batch", "merge_many"):
+            assert getattr(v, member) == _fn_addr(f"kbz_{name}_{member}"), (name, member)
+        assert v.get_module_info is None and v.get_edges is None
+        C.CDLL(None).free(vt)
+    assert not L.kbz_instrumentation_factory(b"afl")
+
+
+@pytest.mark.parametrize("name", P.PLUGINS)
+def test_state_roundtrip_without_gpu(name):
+    rng = np.random.default_rng(3)
+    maps = {"virgin_bits": rng.integers(0, 256, M).astype(np.uint8)}
+    if name == "afl_gpu":
+        maps["virgin_tmout"] = rng.integers(0, 256, M).astype(np.uint8)
+        maps["virgin_crash"] = rng.integers(0, 256, M).astype(np.uint8)
+    else:
+        maps["last_shm_hash"] = 0xDEADBEEF
+    st = P.state_json(maps, M)
+    p = P.Plugin(name, f'{{"map_size": {M}, "max_batch": 8}}', st)
+    back = P.state_maps(p.get_state(), M)
+    for k, v in maps.items():
+        if k == "last_shm_hash":
+            assert back[k] == v
+        else:
+            np.testing.assert_array_equal(back[k], v)
+    # fresh state: all-0xff maps (setup_shm afl_instrumentation.c:555-559)
+    q = P.Plugin(name, f'{{"map_size": {M}}}')
+    assert (P.state_maps(q.get_state(), M)["virgin_bits"] == 0xFF).all()
+    # reference error values
+    assert q.is_new_path() == -1            # before any exec
+    assert q.get_fuzz_result() == P.FUZZ_ERROR
+    assert q.enable() == -1 and "process control" in P.last_error()
+    assert q.is_process_done() == -1
+    assert q.set_state('{"map_size": 8192}') != 0
+    assert q.set_state('{"virgin_bits": "zz"}') != 0
+
+
+def test_bad_options_and_ignore_file(tmp_path):
+    with pytest.raises(RuntimeError):
+        P.Plugin("afl_gpu", '{"map_size": 1000}')
+    bad = tmp_path / "ign.bin"
+    bad.write_bytes(b"\0" * (M - 1))
+    with pytest.raises(RuntimeError, match="Incorrect size"):
+        P.Plugin("dynamorio_gpu", f'{{"map_size": {M}, "ignore_bytes_file": "{bad}"}}')
+    good = tmp_path / "ign2.bin"
+    good.write_bytes(b"\0" * M)
+    P.Plugin("dynamorio_gpu", f'{{"map_size": {M}, "ignore_bytes_file": "{good}"}}').close()
+
+
+def test_no_cpu_fallback():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    p = P.Plugin("afl_gpu", f'{{"map_size": {M}}}')
+    t = np.zeros(M, np.uint8)
+    t[5] = 1
+    assert p.record(t, P.FUZZ_NONE) == 0
+    assert p.is_new_path() == -1  # the triage needs the GPU: it fails, nothing computes on CPU
+    assert P.last_error()
+    q = P.Plugin("afl_gpu", f'{{"map_size": {M}}}')
+    with pytest.raises(RuntimeError, match="merge"):
+        p.merge(q)
+
+
+# ---- GPU ----------------------------------------------------------------------------------------
+
+def _expected(mode, t, oc, virgin=None, ignore=None, last=0):
+    return oracle.triage_batch(mode, t, oc, virgin=virgin, ignore=ignore, last_hash=last,
+                               want=oracle.WANT_H32 | oracle.WANT_X64)
+
+
+MODES = [("afl_gpu", oracle.MODE_AFL), ("dynamorio_gpu", oracle.MODE_DYNAMORIO)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,mode", MODES)
+def test_per_exec_like_fuzzer_main(gpu, name, mode):
+    """fuzzer/main.c:374-385: one exec, then is_new_path; repeated."""
+    t, oc = synth.sparse_np(150, M, seed=21, hot_frac=0.05, outcome_p=(0.8, 0.1, 0.1))
+    t[40] = t[39]
+    oc[40] = oc[39]
+    exp = _expected(mode, t, oc)
+    p = P.Plugin(name, f'{{"map_size": {M}, "max_batch": 16}}')
+    for j in range(t.shape[0]):
+        ticket = p.record(t[j], int(oc[j]))
+        assert ticket == j
+        assert p.is_new_path() == int(exp["hnb"][j] != 0), j
+        assert p.result(ticket) == exp["hnb"][j]
+        assert p.get_fuzz_result() == oc[j]
+    got = P.state_maps(p.get_state(), M)
+    np.testing.assert_array_equal(got["virgin_bits"], exp["virgin"][0])
+    if name == "afl_gpu":
+        np.testing.assert_array_equal(got["virgin_tmout"], exp["virgin"][1])
+        np.testing.assert_array_equal(got["virgin_crash"], exp["virgin"][2])
+    else:
+        assert got["last_shm_hash"] == exp["last_hash"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,mode", MODES)
+def test_deferred_and_batched(gpu, name, mode):
+    t, oc = synth.sparse_np(300, M, seed=22, hot_frac=0.05, outcome_p=(0.8, 0.1, 0.1))
+    exp = _expected(mode, t, oc)
+    p = P.Plugin(name, f'{{"map_size": {M}, "max_batch": 512}}')
+    tickets = [p.record(t[j], int(oc[j])) for j in range(100)]  # queued, not yet triaged
+    got = [p.result(k) for k in tickets]                         # one GPU batch of 100
+    np.testing.assert_array_equal(np.array(got, np.uint8), exp["hnb"][:100])
+    r = p.triage_batch(t[100:], oc[100:])                        # appended batched member
+    np.testing.assert_array_equal(r["hnb"], exp["hnb"][100:])
+    np.testing.assert_array_equal(r["h32"], exp["h32"][100:])
+    np.testing.assert_array_equal(r["x64"], exp["x64"][100:])
+    np.testing.assert_array_equal(P.state_maps(p.get_state(), M)["virgin_bits"], exp["virgin"][0])
+
+
+@pytest.mark.gpu
+def test_dynamorio_ignore_file(gpu, tmp_path):
+    rng = np.random.default_rng(4)
+    ign = np.where(rng.random(M) < 0.4, 0, rng.integers(1, 256, M)).astype(np.uint8)
+    f = tmp_path / "ignore.bin"
+    f.write_bytes(ign.tobytes())
+    t, oc = synth.sparse_np(120, M, seed=23, hot_frac=0.05)
+    exp = _expected(oracle.MODE_DYNAMORIO, t, oc, ignore=ign)
+    p = P.Plugin("dynamorio_gpu", f'{{"map_size": {M}, "ignore_bytes_file": "{f}"}}')
+    r = p.triage_batch(t, oc)
+    np.testing.assert_array_equal(r["hnb"], exp["hnb"])
+    np.testing.assert_array_equal(r["h32"], exp["h32"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,mode", MODES)
+def test_state_load_continue_and_merge(gpu, name, mode):
+    t, oc = synth.sparse_np(200, M, seed=24, hot_frac=0.05, outcome_p=(0.8, 0.1, 0.1))
+    a = P.Plugin(name, f'{{"map_size": {M}}}')
+    a.triage_batch(t[:100], oc[:100])
+    # -isf/-isd style: dump, load into a new state, continue (fuzzer/main.c:300-322, :426-436)
+    b = P.Plugin(name, f'{{"map_size": {M}}}', a.get_state())
+    r = b.triage_batch(t[100:], oc[100:])
+    whole = _expected(mode, t, oc)
+    np.testing.assert_array_equal(r["hnb"], whole["hnb"][100:])
+    # merger: AND of the maps (afl_merge :123-140, dynamorio_merge :1180-1231)
+    c = P.Plugin(name, f'{{"map_size": {M}}}')
+    c.triage_batch(t[50:], oc[50:])
+    m2 = a.merge(c)
+    mm = P.Plugin.merge_many([a, b, c])
+    va, vb, vc = (P.state_maps(x.get_state(), M) for x in (a, b, c))
+    for k in va:
+        if k == "last_shm_hash":
+            continue
+        np.testing.assert_array_equal(P.state_maps(m2.get_state(), M)[k], va[k] & vc[k])
+        np.testing.assert_array_equal(P.state_maps(mm.get_state(), M)[k], va[k] & vb[k] & vc[k])
+    if name == "dynamorio_gpu":
+        assert P.state_maps(mm.get_state(), M)["last_shm_hash"] == 0
