@@ -43,7 +43,19 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--seed", type=int, default=0x5EED)
-    return p.parse_args()
+    p.add_argument("--workload", default="config2",
+                   choices=["config2", "config3", "merge", "stream"],
+                   help="config2 (default, the headline): 65,536 sparse x 64 KiB; config3: "
+                        "16,384 dense x 1 MiB; merge: 100k merger states AND-folded; stream: "
+                        "config2 traces from host memory through the pinned ring (PCIe-bound)")
+    p.add_argument("--states", type=int, default=100000, help="merge workload: states")
+    a = p.parse_args()
+    if a.workload == "config3":
+        if a.batch == 65536:
+            a.batch = 16384
+        if a.map_size == 65536:
+            a.map_size = 1 << 20
+    return a
 
 
 def cpu_baseline(traces_dev, mode, seconds):
@@ -111,6 +123,10 @@ def cpu_baseline_all_cores(traces_dev, mode, seconds):
 
 def main():
     args = parse()
+    if args.workload == "merge":
+        return main_merge(args)
+    if args.workload == "stream":
+        return main_stream(args)
     import torch
     import torch.distributed as dist
 
@@ -130,8 +146,9 @@ def main():
     B, M = args.batch, args.map_size
 
     pool = []
+    gen = synth.dense_torch if args.workload == "config3" else synth.sparse_torch
     for p in range(args.pool):
-        t, oc = synth.sparse_torch(B, M, seed=args.seed + 7919 * p + 104729 * rank, device=dev)
+        t, oc = gen(B, M, seed=args.seed + 7919 * p + 104729 * rank, device=dev)
         pool.append((t, oc))
     ctx = TriageContext(M, mode, B)
     out = {"hnb": torch.empty(B, dtype=torch.uint8, device=dev),
@@ -213,8 +230,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (SURVEY.md §8(d) config 2 generator, seeded, generated in HBM)",
-        "config": {"workload": f"config2: {B} sparse traces/GPU x {M} B map, {args.mode} "
+        "data": f"synthetic (SURVEY.md §8(d) {args.workload} generator, seeded, generated in HBM)",
+        "config": {"workload": f"{args.workload}: {B} "
+                               f"{'dense' if args.workload == 'config3' else 'sparse'} "
+                               f"traces/GPU x {M} B map, {args.mode} "
                                "classify+hash32+last-hash skip+has_new_bits, virgin carried",
                    "map_size": M, "batch_per_gpu": B, "global_batch": world * B,
                    "mode": args.mode, "parallelism": f"shard{world}"},
@@ -234,6 +253,118 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def _timed(fn, steps, warmup):
+    import torch
+
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ev = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        ev.append((a, b))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return el, sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+
+
+def main_merge(args):
+    """BASELINE config 4: N client states (3 virgin maps of 64 KiB each) AND-folded into one
+    (merger/merger.c:79-99), states resident in HBM; one step = one fold of all N.  Each state
+    is all-0xff with random bits cleared (AND of 6 random bytes: P(clear) = 1/64)."""
+    import torch
+
+    from killerbeez_amd.triage import merge_and
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    n, sb = args.states, 3 * 65536
+    states = torch.empty((n, sb), dtype=torch.uint8, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed)
+    for lo in range(0, n, 2000):
+        hi = min(n, lo + 2000)
+        clr = torch.randint(0, 256, (hi - lo, sb), dtype=torch.uint8, device=dev, generator=g)
+        for _ in range(5):
+            clr &= torch.randint(0, 256, (hi - lo, sb), dtype=torch.uint8, device=dev,
+                                 generator=g)
+        states[lo:hi] = ~clr
+    out = torch.empty(sb, dtype=torch.uint8, device=dev)
+    el, ms = _timed(lambda: merge_and(states, out=out), args.steps, args.warmup)
+    torch.cuda.synchronize()
+    # size-independent property: the fold equals the AND of the folds of the two halves
+    halves = merge_and(states[: n // 2]) & merge_and(states[n // 2:])
+    if not torch.equal(halves, out):
+        raise SystemExit("merge self-check failed")
+    bytes_ = n * sb
+    res = {"metric": "merger states AND-folded/sec (3 x 64 KiB virgin maps per state)",
+           "value": round(n * args.steps / el, 1), "unit": "states/s", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(1e3 * el / args.steps, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic merger states (all-0xff, bits cleared w.p. 1/64), generated in HBM",
+           "config": {"workload": f"config4: {n} states x {sb} B, one AND-fold per step",
+                      "states": n, "state_bytes": sb, "parallelism": "shard1"},
+           "roofline": {"bound": "hbm", "achieved": round(bytes_ / (ms * 1e-3) / 1e9, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(bytes_ / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": None, "kernel": "k_and_groups + k_and_rows (one fold)",
+                        "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": bytes_}}
+    if not args.no_cpu:
+        import oracle
+
+        sample = states[:2000].cpu().numpy()
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_seconds:
+            oracle.merge_many(sample)
+            done += sample.shape[0]
+        el_c = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": done / el_c, "unit": "states/s", "cores": 1,
+                               "kind": "port",
+                               "sample": f"2000 states of the workload, AND-folded repeatedly "
+                                         f"({el_c:.1f} s), oracle kbzo_merge_many, 1 thread"}
+    print(json.dumps(res), flush=True)
+
+
+def main_stream(args):
+    """BASELINE config 5 (1 GPU): config-2 traces in pageable host memory, triaged through
+    kbz_triage_batch_host (pinned ring, double-buffered hipMemcpyAsync).  PCIe-bound; this is
+    the PCIe-inclusive rate DESIGN.md quotes, never the headline value."""
+    import torch
+
+    from killerbeez_amd import synth
+    from killerbeez_amd.triage import MODES, WANT_H32, TriageContext
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    B, M = min(args.batch, 16384), args.map_size
+    t, oc = synth.sparse_torch(B, M, seed=args.seed, device=dev)
+    host, hoc = t.cpu().numpy(), oc.cpu().numpy()
+    del t, oc
+    ctx = TriageContext(M, MODES[args.mode], B)
+    for _ in range(args.warmup):
+        ctx.triage_host(host, hoc, WANT_H32)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.triage_host(host, hoc, WANT_H32)
+    el = time.perf_counter() - t0
+    res = {"metric": "traces triaged/sec from host memory (64KB map, PCIe-inclusive)",
+           "value": round(B * args.steps / el, 1), "unit": "traces/s", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(1e3 * el / args.steps, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic config-2 traces in pageable host memory",
+           "config": {"workload": f"stream: {B} sparse traces x {M} B per step via the pinned "
+                                  "ring", "batch": B, "map_size": M, "mode": args.mode},
+           "pcie_GBps": round(B * M * args.steps / el / 1e9, 2)}
+    print(json.dumps(res), flush=True)
+    ctx.close()
 
 
 if __name__ == "__main__":
