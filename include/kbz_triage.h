@@ -162,6 +162,27 @@ int kbz_xxh64_device(const uint8_t *rows, size_t n, size_t stride, size_t len, u
 /* Synchronise the context's work and report any device-side consistency error (-1). */
 int kbz_sync(kbz_ctx_t *ctx, void *stream);
 
+/* ---- unique crash/hang table: insert-if-absent set of 16-byte keys -------------------------- */
+/* The reference's hash-set novelty (linux_ipt_instrumentation.c:412-424: HASH_FIND, HASH_ADD
+ * when absent, new iff absent; insertion-ordered like uthash) applied to an ordered batch:
+ * key j is new iff it is absent from the set and from keys 0..j-1 of the batch.  Keys are two
+ * uint64 words like the IPT key {tip, tnt} (linux_ipt_instrumentation.h:19-22); for trace dedup
+ * {XXH64 of the transformed trace (kbz_triage_batch_* x64_out), outcome class}. */
+typedef struct kbz_set kbz_set_t;
+/* capacity: most keys the set will hold (table = 2x, power of two). */
+kbz_set_t *kbz_set_create(size_t capacity);
+void kbz_set_destroy(kbz_set_t *set);
+const char *kbz_set_last_error(void);
+/* keys: device uint64[2*n]; mask: device uint8[n] or NULL (rows with mask 0 are neither
+ * inserted nor new); is_new_out: device uint8[n] (1 = new, inserted).  Stream-ordered. */
+int kbz_set_insert_device(kbz_set_t *set, const uint64_t *keys, const uint8_t *mask, size_t n,
+                          uint8_t *is_new_out, void *stream);
+/* Number of keys in the set; -1 if the capacity was exceeded (keys dropped).  Synchronous. */
+int kbz_set_size(kbz_set_t *set, size_t *out);
+/* The first min(cap, size) keys in insertion order into host uint64[2*cap]; *n_out = size.
+ * Synchronous. */
+int kbz_set_keys(kbz_set_t *set, uint64_t *host_out, size_t cap, size_t *n_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -41,6 +41,12 @@ SIGNATURES = [
     ("kbz_hash32_device", _i, [_vp, _sz, _sz, _sz, _u32, _vp, _vp]),
     ("kbz_xxh64_device", _i, [_vp, _sz, _sz, _sz, _u64, _vp, _vp]),
     ("kbz_sync", _i, [_vp, _vp]),
+    ("kbz_set_create", _vp, [_sz]),
+    ("kbz_set_destroy", None, [_vp]),
+    ("kbz_set_last_error", C.c_char_p, []),
+    ("kbz_set_insert_device", _i, [_vp, _vp, _vp, _sz, _vp, _vp]),
+    ("kbz_set_size", _i, [_vp, C.POINTER(_sz)]),
+    ("kbz_set_keys", _i, [_vp, _vp, _sz, C.POINTER(_sz)]),
 ]
 
 

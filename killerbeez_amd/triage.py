@@ -268,3 +268,65 @@ def xxh64_rows(rows, length=None, seed=0, stream=None):
                                  C.c_void_p(out.data_ptr()), _stream_handle(stream)),
           "kbz_xxh64_device")
     return out
+
+
+class UniqueSet:
+    """Insert-if-absent set of 16-byte keys on the GPU (kbz_set_*; the reference's hash-set
+    novelty, linux_ipt_instrumentation.c:412-424): the unique crash/hang table."""
+
+    def __init__(self, capacity: int):
+        L = lib()
+        self._h = L.kbz_set_create(int(capacity))
+        if not self._h:
+            raise KbzError("kbz_set_create: " + (L.kbz_set_last_error() or b"").decode())
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().kbz_set_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise KbzError(f"{what}: {(lib().kbz_set_last_error() or b'').decode()}")
+
+    def insert(self, keys, mask=None, stream=None):
+        """keys: CUDA int64 tensor [n, 2]; mask: CUDA bool/uint8 [n] or None.  Returns CUDA uint8
+        [n]: 1 where the key was new (and is now in the set)."""
+        import torch
+
+        keys = keys.contiguous()
+        n = keys.shape[0]
+        out = torch.empty(n, dtype=torch.uint8, device=keys.device)
+        m = None if mask is None else mask.to(torch.uint8).contiguous()
+        self._check(lib().kbz_set_insert_device(
+            self._h, C.c_void_p(keys.data_ptr()) if n else None,
+            None if m is None else C.c_void_p(m.data_ptr()), n,
+            C.c_void_p(out.data_ptr()) if n else None, _stream_handle(stream)),
+            "kbz_set_insert_device")
+        return out
+
+    def size(self) -> int:
+        x = C.c_size_t()
+        self._check(lib().kbz_set_size(self._h, C.byref(x)), "kbz_set_size")
+        return x.value
+
+    def keys(self) -> np.ndarray:
+        """All keys in insertion order, uint64 [size, 2]."""
+        n = self.size()
+        out = np.zeros((max(n, 1), 2), np.uint64)
+        got = C.c_size_t()
+        self._check(lib().kbz_set_keys(self._h, _np_ptr(out), n, C.byref(got)), "kbz_set_keys")
+        return out[:got.value]
+
+
+def dedup_keys(x64, outcome):
+    """Keys {XXH64 of the transformed trace, outcome class} for UniqueSet (CUDA int64 [n, 2])."""
+    import torch
+
+    return torch.stack([x64.to(torch.int64), outcome.to(torch.int64)], dim=1)
