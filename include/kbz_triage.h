@@ -135,7 +135,8 @@ int kbz_shard_reduce(kbz_ctx_t *ctx, void *stream);
  * 3 otherwise) into device memory d_out. */
 int kbz_shard_aggregate(kbz_ctx_t *ctx, uint8_t *d_out, void *stream);
 size_t kbz_shard_aggregate_bytes(kbz_ctx_t *ctx);
-/* prefix/total: device, nclass*map_size bytes each (prefix may be NULL = all zero). */
+/* prefix/total: device, nclass*map_size bytes each (prefix may be NULL = all zero; total may be
+ * NULL = this shard's own aggregate, i.e. a single-shard batch). */
 int kbz_shard_finish(kbz_ctx_t *ctx, const uint8_t *prefix, const uint8_t *total,
                      uint8_t *hnb_out, void *stream);
 

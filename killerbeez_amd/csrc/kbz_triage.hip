@@ -468,53 +468,53 @@ __global__ void k_skip(const uint32_t *h32, const uint8_t *neq, uint32_t n,
   }
 }
 
-// Recompute chunk ORs (DynamoRIO class 0) without skipped traces, for listed chunks.
-__global__ __launch_bounds__(256) void k_fixchunk(const uint8_t *traces, size_t stride, uint32_t n,
-                                                   uint32_t map_size, const uint8_t *skip,
-                                                   const uint32_t *fix_list,
-                                                   const uint32_t *fix_cnt, uint8_t *chunk_or) {
-  const uint32_t ncol = map_size / 16, cnt = *fix_cnt;
-  for (size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x; w < (size_t)cnt * ncol;
-       w += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t chunk = fix_list[w / ncol];
-    const uint32_t col = (uint32_t)(w % ncol) * 16;
+// DynamoRIO fix path of the skip rule, for k_total: chunks listed by k_skip hold a skipped trace
+// that differs from its predecessor, so their ORs (class 0) are recomputed without the skipped
+// traces, and so are the aggregates of their segments.  One thread owns one 8-byte column of
+// every listed chunk and segment, so no other thread's result is needed (usually no chunk is
+// listed and this costs one load).
+struct FixArgs {
+  const uint8_t *traces;
+  size_t stride;
+  uint32_t n;
+  const uint8_t *skip;
+  const uint32_t *fix_list;
+  const uint32_t *fix_cnt;
+  uint8_t *chunk_or;
+  const uint8_t *chunk_cls;
+  uint32_t nchunks, seg_len;
+};
+__device__ void fix_column(const FixArgs &f, uint32_t map_size, uint32_t col, uint8_t *segor) {
+  const uint32_t cnt = *f.fix_cnt;
+  for (uint32_t i = 0; i < cnt; i++) {
+    const uint32_t chunk = f.fix_list[i];
     const uint64_t row0 = (uint64_t)chunk * kChunk;
-    const int nrows = (int)min((uint64_t)kChunk, (uint64_t)n - row0);
-    uint4 acc = make_uint4(0, 0, 0, 0);
-    for (int r = 0; r < nrows; r++) {
-      if (skip[row0 + r]) continue;
-      acc = or4(acc, classify16(*(const uint4 *)(traces + (row0 + r) * stride + col)));
-    }
-    *(uint4 *)(chunk_or + (size_t)chunk * map_size + col) = acc;
+    const int nrows = (int)min((uint64_t)kChunk, (uint64_t)f.n - row0);
+    uint64_t acc = 0;
+    for (int r = 0; r < nrows; r++)
+      if (!f.skip[row0 + r]) acc |= classify8(*(const uint64_t *)(f.traces + (row0 + r) * f.stride + col));
+    *(uint64_t *)(f.chunk_or + (size_t)chunk * map_size + col) = acc;
   }
-}
-
-// Recompute the segment aggregates of segments holding a listed chunk (idempotent).
-__global__ __launch_bounds__(256) void k_segfix(const uint8_t *chunk_or, const uint8_t *chunk_cls,
-                                                 uint32_t nchunks, uint32_t seg_len,
-                                                 uint32_t map_size, const uint32_t *fix_list,
-                                                 const uint32_t *fix_cnt, uint8_t *segor) {
-  const uint32_t ncol = map_size / 16, cnt = *fix_cnt;
-  for (size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x; w < (size_t)cnt * ncol;
-       w += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t seg = fix_list[w / ncol] / seg_len;
-    const uint32_t col = (uint32_t)(w % ncol) * 16;
-    const uint32_t c0 = seg * seg_len, c1 = min(nchunks, c0 + seg_len);
-    uint4 acc = make_uint4(0, 0, 0, 0);
+  for (uint32_t i = 0; i < cnt; i++) {  // idempotent when two listed chunks share a segment
+    const uint32_t seg = f.fix_list[i] / f.seg_len;
+    const uint32_t c0 = seg * f.seg_len, c1 = min(f.nchunks, c0 + f.seg_len);
+    uint64_t acc = 0;
     for (uint32_t c = c0; c < c1; c++)
-      if (chunk_cls[c] & 1) acc = or4(acc, *(const uint4 *)(chunk_or + (size_t)c * map_size + col));
-    *(uint4 *)(segor + (size_t)seg * map_size + col) = acc;
+      if (f.chunk_cls[c] & 1) acc |= *(const uint64_t *)(f.chunk_or + (size_t)c * map_size + col);
+    *(uint64_t *)(segor + (size_t)seg * map_size + col) = acc;
   }
 }
 
-// Per column (8 B per thread): segprev[s] = OR of segments < s (local exclusive prefix),
-// total = OR of all segments; segor is re-zeroed for the next batch.
+// Per column (8 B per thread): [DynamoRIO: fix path first], then segprev[s] = OR of segments
+// < s (local exclusive prefix), total = OR of all segments; segor is re-zeroed for the next
+// batch.
 __global__ __launch_bounds__(256) void k_total(uint8_t *segor, uint32_t nseg, int nclass,
                                                 uint32_t map_size, uint8_t *segprev,
-                                                uint8_t *total) {
+                                                uint8_t *total, FixArgs fix) {
   const uint32_t col = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
   const int k = blockIdx.z;
   if (col >= map_size) return;
+  if (fix.fix_cnt && k == 0) fix_column(fix, map_size, col, segor);
   uint64_t v[kMaxSeg];
 #pragma unroll
   for (int s = 0; s < kMaxSeg; s++)  // all loads in flight at once
@@ -610,6 +610,10 @@ __global__ __launch_bounds__(256) void k_scan(const uint8_t *chunk_or, const uin
     const uint4 t = *(const uint4 *)(gtotal + kc);
     *(uint4 *)(vnext + kc) = make_uint4(vir.x & ~(t.x & rel.x), vir.y & ~(t.y & rel.y),
                                         vir.z & ~(t.z & rel.z), vir.w & ~(t.w & rel.w));
+    if (k == nclass - 1)  // maps this mode does not use (DynamoRIO: tmout, crash) carry over
+      for (int kk = nclass; kk < 3; kk++)
+        *(uint4 *)(vnext + (size_t)kk * map_size + col) =
+            *(const uint4 *)(vcur + (size_t)kk * map_size + col);
   }
   const uint4 vr = live ? make_uint4(vir.x & rel.x, vir.y & rel.y, vir.z & rel.z, vir.w & rel.w)
                         : make_uint4(0, 0, 0, 0);
@@ -678,9 +682,20 @@ __global__ __launch_bounds__(256) void k_resolve(const uint8_t *traces, size_t s
   }
 }
 
+// Per-trace outputs, then re-arm the per-batch state for the next batch (no memsets between
+// batches): hnb32, the item and fix-list counters (the sticky error flags counters[1..2] stay
+// until kbz_sync reports them), the fix-list flags and the shard's last-hash pair.
 __global__ void k_pack(uint32_t *hnb32, const uint32_t *h32, uint32_t n, uint8_t *hnb_out,
-                       uint32_t *h32_out) {
+                       uint32_t *h32_out, uint32_t *counters, uint32_t *flags, uint32_t nchunks,
+                       uint32_t *shard_last) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < nchunks && flags) flags[j] = 0;
+  if (j == 0) {
+    counters[0] = 0;
+    counters[3] = 0;
+    shard_last[0] = 0;
+    shard_last[1] = 0;
+  }
   if (j >= n) return;
   if (hnb_out) hnb_out[j] = (uint8_t)hnb32[j];
   if (h32_out) h32_out[j] = h32[j];
@@ -852,6 +867,7 @@ struct kbz_ctx {
   uint32_t *cur_h32_out = nullptr;
   uint32_t *cur_h32 = nullptr;  // where pass 1 wrote this shard's hashes
   uint32_t cur_chunks = 0, cur_seg_len = 1, cur_nseg = 1;
+  bool fix_pending = false;  // DynamoRIO: k_skip ran for this batch, k_total runs the fix path
   int stage = 0;
   // host streaming
   hipStream_t copy_stream = nullptr, work_stream = nullptr;
@@ -1026,6 +1042,7 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   (void)hipMemset(c->V[0], 0xff, 3 * M);
   (void)hipMemset(c->last, 0, 2 * sizeof(uint32_t));
   (void)hipMemset(c->counters, 0, 8 * sizeof(uint32_t));
+  (void)hipMemset(c->shard_last, 0, 2 * sizeof(uint32_t));
   // consumers re-zero these for the next batch (k_total: segor, k_pack: hnb32)
   (void)hipMemset(c->segor, 0, kMaxSeg * nc * M);
   (void)hipMemset(c->hnb32, 0, max_batch * sizeof(uint32_t));
@@ -1100,8 +1117,9 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
   c->cur_nseg = std::max(1u, std::min<unsigned>(kMaxSeg, c->cur_chunks));
   c->cur_seg_len = std::max(1u, cdiv(c->cur_chunks, c->cur_nseg));
   c->cur_nseg = std::max(1u, cdiv(c->cur_chunks, c->cur_seg_len));
-  HIP_TRY(hipMemsetAsync(c->counters, 0, 8 * sizeof(uint32_t), s));
-  HIP_TRY(hipMemsetAsync(c->shard_last, 0, 2 * sizeof(uint32_t), s));
+  c->fix_pending = false;
+  // counters[0], counters[3], flags and shard_last are zero here: k_pack of the previous
+  // batch (or context creation) re-armed them
   if (n == 0) {
     c->stage = 1;
     return 0;
@@ -1150,17 +1168,7 @@ int kbz_shard_link(kbz_ctx_t *c, const uint32_t *prev_last, int is_first,
                        c->flags, c->fix_list, c->counters + 3);
     HIP_TRY(hipGetLastError());
     c->lcur = nl;
-    if (n) {
-      // rarely-taken path: both kernels exit at once when the fix list is empty
-      hipLaunchKernelGGL(k_fixchunk, dim3(256), dim3(256), 0, s, c->cur_traces, c->cur_stride,
-                         (uint32_t)n, (uint32_t)c->M, c->skip, c->fix_list, c->counters + 3,
-                         c->chunk_or);
-      HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_segfix, dim3(256), dim3(256), 0, s, c->chunk_or, c->chunk_cls,
-                         c->cur_chunks, c->cur_seg_len, (uint32_t)c->M, c->fix_list,
-                         c->counters + 3, c->segor);
-      HIP_TRY(hipGetLastError());
-    }
+    c->fix_pending = n != 0;  // k_total runs the (usually empty) fix path
   }
   c->stage = 2;
   return 0;
@@ -1174,8 +1182,21 @@ int kbz_shard_reduce(kbz_ctx_t *c, void *stream) {
     HIP_TRY(hipMemsetAsync(c->total, 0, c->nc * c->M, s));
     HIP_TRY(hipMemsetAsync(c->segprev, 0, c->nc * c->M, s));
   } else {
+    FixArgs fx{};
+    if (c->fix_pending) {
+      fx.traces = c->cur_traces;
+      fx.stride = c->cur_stride;
+      fx.n = (uint32_t)c->cur_n;
+      fx.skip = c->skip;
+      fx.fix_list = c->fix_list;
+      fx.fix_cnt = c->counters + 3;
+      fx.chunk_or = c->chunk_or;
+      fx.chunk_cls = c->chunk_cls;
+      fx.nchunks = c->cur_chunks;
+      fx.seg_len = c->cur_seg_len;
+    }
     hipLaunchKernelGGL(k_total, dim3(cdiv(c->M / 8, 256), 1, c->nc), dim3(256), 0, s, c->segor,
-                       c->cur_nseg, c->nc, (uint32_t)c->M, c->segprev, c->total);
+                       c->cur_nseg, c->nc, (uint32_t)c->M, c->segprev, c->total, fx);
     HIP_TRY(hipGetLastError());
   }
   c->stage = 3;
@@ -1195,7 +1216,7 @@ size_t kbz_shard_aggregate_bytes(kbz_ctx_t *c) { return c ? c->nc * c->M : 0; }
 int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, uint8_t *hnb_out,
                      void *stream) {
   if (!c || c->stage != 3) return fail("kbz_shard_finish: call kbz_shard_reduce first");
-  if (!total) return fail("kbz_shard_finish: total is required");
+  if (!total) total = c->total;  // single shard: its own aggregate is the total
   DevGuard g(c->device);
   hipStream_t s = (hipStream_t)stream;
   const unsigned gx = cdiv(c->M / 16, 256);
@@ -1206,9 +1227,6 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
                      c->cur_chunks, c->cur_seg_len, c->nc, (uint32_t)c->M, c->segprev, prefix,
                      total, c->V[c->vcur], c->V[vn], ign, c->items, c->item_cap, c->counters);
   HIP_TRY(hipGetLastError());
-  if (c->nc < 3)  // DYNAMORIO: tmout/crash maps are carried unchanged
-    HIP_TRY(hipMemcpyAsync(c->V[vn] + c->nc * c->M, c->V[c->vcur] + c->nc * c->M,
-                           (3 - c->nc) * c->M, hipMemcpyDeviceToDevice, s));
   if (c->cur_n) {
     hipLaunchKernelGGL(k_resolve, dim3(512), dim3(256), 0, s, c->cur_traces, c->cur_stride,
                        (uint32_t)c->cur_n, c->mode, c->cur_outcome,
@@ -1217,10 +1235,14 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_pack, dim3(cdiv(c->cur_n, 256)), dim3(256), 0, s, c->hnb32, c->cur_h32,
                        (uint32_t)c->cur_n, hnb_out ? hnb_out : (uint8_t *)nullptr,
-                       (c->cur_h32_out && c->cur_h32_out != c->cur_h32) ? c->cur_h32_out : nullptr);
+                       (c->cur_h32_out && c->cur_h32_out != c->cur_h32) ? c->cur_h32_out : nullptr,
+                       c->counters, c->mode == KBZ_MODE_DYNAMORIO ? c->flags : nullptr,
+                       c->cur_chunks, c->shard_last);
     HIP_TRY(hipGetLastError());
-    if (c->mode == KBZ_MODE_DYNAMORIO)  // re-arm the fix-list flags of this batch
-      HIP_TRY(hipMemsetAsync(c->flags, 0, c->cur_chunks * sizeof(uint32_t), s));
+  } else {
+    // empty shard: k_skip may still have written the fix count / shard pair; re-arm them
+    HIP_TRY(hipMemsetAsync(c->counters + 3, 0, sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(c->shard_last, 0, 2 * sizeof(uint32_t), s));
   }
   c->vcur = vn;
   c->stage = 0;
@@ -1262,8 +1284,10 @@ int kbz_sync(kbz_ctx_t *c, void *stream) {
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   uint32_t cnt[4];
   HIP_TRY(hipMemcpy(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost));
-  if (cnt[1]) return fail("claim list overflow");
-  if (cnt[2]) return fail("inconsistent claim (internal error)");
+  if (cnt[1] || cnt[2]) {  // sticky until reported here
+    HIP_TRY(hipMemset(c->counters + 1, 0, 2 * sizeof(uint32_t)));
+    return fail(cnt[1] ? "claim list overflow" : "inconsistent claim (internal error)");
+  }
   return 0;
 }
 

@@ -205,8 +205,8 @@ class TriageContext:
 
     def shard_finish(self, prefix, total, stream=None):
         out = self._out
-        check(lib().kbz_shard_finish(self._h, None if prefix is None else C.c_void_p(prefix.data_ptr()),
-                                     C.c_void_p(total.data_ptr()), C.c_void_p(out["hnb"].data_ptr()),
+        ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        check(lib().kbz_shard_finish(self._h, ptr(prefix), ptr(total), ptr(out["hnb"]),
                                      _stream_handle(stream)), "kbz_shard_finish")
         return out
 
