@@ -582,14 +582,18 @@ __device__ __forceinline__ void emit_items_wave(uint32_t chunk, int k, uint32_t 
 // Per (segment, 16-B column group): walk the segment's chunks in order with the running OR
 // `prev` (seeded with the OR of earlier segments and earlier shards); bits a chunk adds
 // that are still virgin become claim items.  Blocks of segment 0 also write V' = V & ~total.
+// A segment whose cumulative OR (segprev of the next segment, or this shard's total for the
+// last one) adds no still-virgin bit over `prev` cannot claim anything: its waves skip the
+// chunk walk (exact; in steady-state fuzzing almost every segment takes this path).
 __global__ __launch_bounds__(256) void k_scan(const uint8_t *chunk_or, const uint8_t *chunk_cls,
                                                uint32_t nchunks, uint32_t seg_len, int nclass,
                                                uint32_t map_size, const uint8_t *segprev,
+                                               uint32_t nseg, const uint8_t *ltotal,
                                                const uint8_t *gprefix, const uint8_t *gtotal,
                                                const uint8_t *vcur, uint8_t *vnext,
                                                const uint8_t *ignore, uint64_t *items,
                                                uint32_t cap, uint32_t *counters) {
-  // no early return: every lane of a wave takes part in the item-allocation prefix
+  // no per-lane early return: every lane of a wave takes part in the item-allocation prefix
   const uint32_t col0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
   const bool live = col0 < map_size;
   const uint32_t col = live ? col0 : 0;
@@ -617,6 +621,11 @@ __global__ __launch_bounds__(256) void k_scan(const uint8_t *chunk_or, const uin
   }
   const uint4 vr = live ? make_uint4(vir.x & rel.x, vir.y & rel.y, vir.z & rel.z, vir.w & rel.w)
                         : make_uint4(0, 0, 0, 0);
+  const uint4 send = *(const uint4 *)((s + 1 < nseg) ? segprev + (size_t)(s + 1) * nclass * map_size + kc
+                                                      : ltotal + kc);
+  const uint32_t seg_new = (send.x & vr.x & ~prev.x) | (send.y & vr.y & ~prev.y) |
+                           (send.z & vr.z & ~prev.z) | (send.w & vr.w & ~prev.w);
+  if (!__ballot(seg_new != 0)) return;  // wave-uniform: nothing new in this segment
   const uint32_t c0 = s * seg_len, c1 = min(nchunks, c0 + seg_len);
   // 8 chunks per batch, loads issued unconditionally (a chunk without traces of class k has a
   // stale row: masked to 0 after the load) so each batch costs one memory round trip
@@ -1224,8 +1233,9 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
   const uint8_t *ign = (c->mode == KBZ_MODE_DYNAMORIO) ? c->ignore : nullptr;
   const uint32_t nseg = c->cur_n ? c->cur_nseg : 1;
   hipLaunchKernelGGL(k_scan, dim3(gx, nseg, c->nc), dim3(256), 0, s, c->chunk_or, c->chunk_cls,
-                     c->cur_chunks, c->cur_seg_len, c->nc, (uint32_t)c->M, c->segprev, prefix,
-                     total, c->V[c->vcur], c->V[vn], ign, c->items, c->item_cap, c->counters);
+                     c->cur_chunks, c->cur_seg_len, c->nc, (uint32_t)c->M, c->segprev, nseg,
+                     c->total, prefix, total, c->V[c->vcur], c->V[vn], ign, c->items,
+                     c->item_cap, c->counters);
   HIP_TRY(hipGetLastError());
   if (c->cur_n) {
     hipLaunchKernelGGL(k_resolve, dim3(512), dim3(256), 0, s, c->cur_traces, c->cur_stride,
