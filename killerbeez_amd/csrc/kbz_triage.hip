@@ -113,6 +113,16 @@ template <int N>
 __device__ __forceinline__ void vmcnt_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// The same wait naming the ring slot's registers "+v" (cdna_hip_programming.md, asm loads form
+// (ii)): no consumer of them, a register copy included, is scheduled above it.
+template <int N>
+__device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[8]) {
+  asm volatile("s_waitcnt vmcnt(%8)"
+               : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
+                 "+v"(r[6]), "+v"(r[7])
+               : "n"(N)
+               : "memory");
+}
 // Drain every asm load, keeping their destination registers live up to the wait: an asm
 // load's output looks ready to the compiler, so once it is dead the compiler may reuse the
 // register while the load is still in flight (the late write would clobber it).
@@ -443,6 +453,222 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
     KBZ_STAMP_FLUSH(chunk * 2 + 1);
     drain_asm_loads(R);
     if (MODE == KBZ_MODE_DYNAMORIO && valid) a.neq[row0 + lane] = neq != 0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// pass 1, wide-map variant (few chunks: a batch of large maps, e.g. BASELINE config 3 with
+// 16,384 x 1 MiB = 256 chunks).  k_pass1s then runs one 2-wave workgroup per CU and is
+// compute-bound twice over (MI355X, config 3: 27.2 ms per batch; 9.3 ms without the transform
+// work, 3.3 ms with neither transform nor chains).  Here the per-word work is spread over
+// NX transform waves and the serial chain is cut to its dependent part:
+//   wave L:      loads rows 0-31 of tile s, and chains tile s-2: per word only the
+//                hash32 step (xor, rotl, *5+C) on the mixed word X computed (+ XXH64 rounds);
+//   wave F:      loads rows 32-63 of tile s (no compute);
+//   waves X_i:   transform tile s-1 (words of slots q with q % NX == i): classify / simplify in
+//                place, column ORs over the 64 traces (DPP), DynamoRIO neighbour equality, and
+//                the per-word hash32 mix k = h32_mix(word & ignore) into the k buffer; they store
+//                their words' column ORs and segment atomics (X waves issue no asm loads, so
+//                their stores disturb no counted wait).
+// A tile lives in buffer s % 3 for three steps (filled, transformed, chained); its k values in
+// kbuf[s % 3], stored [slot][row][2] so both the writes (lane = row) and L's row-per-lane
+// ds_read_b128 are conflict-free.  Steps s = 0..ntiles+1, rounded up to a multiple of D, one
+// barrier each.  Same vmcnt accounting as k_pass1s for L and F (only their NLD loads per step).
+// LDS 98 KiB: one workgroup per CU, 2+NX waves.
+// ---------------------------------------------------------------------------------------------
+template <int MODE, bool IGN, bool X64, int NX, int D = 2>
+__global__ __launch_bounds__(64 * (2 + NX), 1) void k_pass1w(Pass1Args a) {
+  constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
+  constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = 8;
+  constexpr int TILE = kChunk * SLOTS;  // uint4 per tile buffer
+  __shared__ uint4 lds[3 * TILE];
+  __shared__ uint4 kbuf[3 * TILE];      // [buf][slot][row] of {k(2q), k(2q+1)}
+  __shared__ uint64_t neqs[NX][kChunk];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const uint32_t chunk = blockIdx.x;
+  const uint64_t row0 = (uint64_t)chunk * kChunk;
+  const int nrows = (int)min((uint64_t)kChunk, (uint64_t)a.n - row0);
+  const bool valid = lane < nrows;
+  const int oc = (valid && a.outcome) ? a.outcome[row0 + lane] : KBZ_FUZZ_NONE;
+  const int cls = class_of(MODE, oc);
+  const int xf = valid ? class_xf(MODE, cls) : XF_RAW;
+  const bool simp = (xf == XF_SIMPLIFY);
+  const uint32_t ntiles = a.map_size / TW;
+  const uint32_t nsteps = ntiles + 2;
+
+  if (wave < 2) {
+    // ------------------------------------------------------------ waves L (0) and F (1)
+    const int lr = lane / SLOTS, ls = lane % SLOTS;
+    const uint8_t *lbase = a.traces + row0 * a.stride + ls * 16;
+    uint32_t roff[NLD];
+#pragma unroll
+    for (int i = 0; i < NLD; i++)
+      roff[i] = (uint32_t)(min(32 * wave + RPI * i + lr, nrows - 1) * a.stride);
+    auto load_half = [&](u32x4 (&r)[NLD], uint32_t t) {  // branch-free (see k_pass1s)
+      const uint32_t msk = t < ntiles ? ~0u : 0u;
+#pragma unroll
+      for (int i = 0; i < NLD; i++) asm_load16(r[i], lbase + ((t * TW + roff[i]) & msk));
+    };
+    auto store_half = [&](const u32x4 (&r)[NLD], int b) {
+#pragma unroll
+      for (int i = 0; i < NLD; i++) {
+        const int rr = 32 * wave + RPI * i + lr;
+        const u32x4 v = r[i];
+        lds[b * TILE + rr * SLOTS + (ls ^ (rr & 15))] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+    };
+    uint64_t h = (uint64_t)(kHashConst ^ a.map_size);
+    uint64_t x0 = kXP1 + kXP2, x1 = kXP2, x2 = 0, x3 = 0 - kXP1;
+    auto chain_tile = [&](uint32_t t) {
+      const int b = t % 3;
+      const uint4 *krow = &kbuf[b * TILE + lane];
+      const uint4 *row = &lds[b * TILE + lane * SLOTS];
+      const int sw = lane & 15;
+#pragma unroll 4
+      for (int q = 0; q < SLOTS; q++) {
+        const uint4 kk = krow[q * kChunk];
+        h = h32_step_fast(h, (uint64_t)kk.x | ((uint64_t)kk.y << 32));
+        h = h32_step_fast(h, (uint64_t)kk.z | ((uint64_t)kk.w << 32));
+        if (X64) {
+          const uint4 v = row[q ^ sw];
+#pragma unroll
+          for (int e = 0; e < 2; e++) {
+            uint64_t tw = ld_u64(v, e);
+            if (simp && tw == 0) tw = kSimpleZero;  // an untransformed zero word (see k_pass1s)
+            const int xl = (2 * q + e) & 3;
+            if (xl == 0) x0 = xx_round(x0, tw);
+            else if (xl == 1) x1 = xx_round(x1, tw);
+            else if (xl == 2) x2 = xx_round(x2, tw);
+            else x3 = xx_round(x3, tw);
+          }
+        }
+      }
+    };
+    u32x4 R[D][NLD];
+#pragma unroll
+    for (int d = 0; d < D; d++) load_half(R[d], d);
+    for (uint32_t g = 0; g < nsteps; g += D) {
+#pragma unroll
+      for (int u = 0; u < D; u++) {
+        const uint32_t s = g + u;
+        if (wave == 0 && s >= 2 && s - 2 < ntiles) chain_tile(s - 2);
+        vmcnt_wait_ring<(D - 1) * NLD>(R[u]);
+        store_half(R[u], s % 3);
+        load_half(R[u], s + D);
+        lds_barrier();
+      }
+    }
+    drain_asm_loads(R);
+    lds_barrier();  // (Z): the X waves' neighbour flags are in neqs
+    if (wave == 0 && valid) {
+      const uint32_t h32 = h32_final(h);
+      a.h32[row0 + lane] = h32;
+      if (X64 && a.x64) {
+        uint64_t xh = rotl64(x0, 1) + rotl64(x1, 7) + rotl64(x2, 12) + rotl64(x3, 18);
+        xh = xx_merge(xh, x0);
+        xh = xx_merge(xh, x1);
+        xh = xx_merge(xh, x2);
+        xh = xx_merge(xh, x3);
+        xh += a.map_size;
+        a.x64[row0 + lane] = xx_avalanche(xh);
+      }
+      if (row0 + lane == (uint64_t)a.n - 1) {
+        a.shard_last[0] = h32;
+        a.shard_last[1] = 1;
+      }
+    }
+    if (wave == 1 && MODE == KBZ_MODE_DYNAMORIO && valid) {
+      uint64_t nq = 0;
+#pragma unroll
+      for (int i = 0; i < NX; i++) nq |= neqs[i][lane];
+      a.neq[row0 + lane] = nq != 0;
+    }
+  } else {
+    // ------------------------------------------------------------ waves X_i
+    const int xi = wave - 2;
+    uint64_t present[NC];
+#pragma unroll
+    for (int k = 0; k < NC; k++) present[k] = __ballot(valid && cls == k);
+    if (xi == 0 && lane == 0) {
+      uint8_t m = 0;
+#pragma unroll
+      for (int k = 0; k < NC; k++) m |= present[k] ? (1u << k) : 0u;
+      a.chunk_cls[chunk] = m;
+    }
+    const uint32_t seg = chunk / a.seg_len;
+    const uint64_t ksimp = h32_mix(kSimpleZero);
+    uint64_t neq = 0;
+    auto transform_tile = [&](uint32_t t) {
+      const int b = t % 3;
+      const uint64_t *ig = IGN ? (const uint64_t *)(a.ignore + (size_t)t * TW) : nullptr;
+      uint4 *row = &lds[b * TILE + lane * SLOTS];
+      uint64_t *krow = (uint64_t *)&kbuf[b * TILE];
+      const int sw = lane & 15;
+      uint64_t orw[NC];
+#pragma unroll
+      for (int k = 0; k < NC; k++) orw[k] = 0;
+      for (int q = xi; q < SLOTS; q += NX) {
+        uint4 *slot = &row[q ^ sw];
+        uint4 v = *slot;
+        bool dirty = false;
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          const int wi = 2 * q + e;
+          const uint64_t x = ld_u64(v, e);
+          uint64_t kw;
+          if (__ballot(x != 0)) {
+            const uint64_t tw = xform8(x, xf);
+            if (e) { v.z = (uint32_t)tw; v.w = (uint32_t)(tw >> 32); }
+            else { v.x = (uint32_t)tw; v.y = (uint32_t)(tw >> 32); }
+            dirty = true;
+            kw = h32_mix(tw & (IGN ? ig[wi] : ~0ull));
+#pragma unroll
+            for (int k = 0; k < NC; k++) {
+              if (present[k]) {
+                const uint64_t r = wave_or64((valid && cls == k) ? tw : 0);
+                orw[k] = (lane == wi) ? r : orw[k];
+              }
+            }
+            if (MODE == KBZ_MODE_DYNAMORIO) {
+              const uint64_t rel = IGN ? ~nonzero_bytes8(ig[wi]) : ~0ull;
+              neq |= (tw ^ from_prev_lane(tw)) & rel;
+            }
+          } else {
+            kw = simp ? ksimp : 0;
+            if (MODE != KBZ_MODE_DYNAMORIO) {
+#pragma unroll
+              for (int k = 1; k < NC; k++)  // simplified classes see 0x01 bytes everywhere
+                if (present[k]) orw[k] = (lane == wi) ? kSimpleZero : orw[k];
+            }
+          }
+          krow[(size_t)q * 2 * kChunk + 2 * lane + e] = kw;
+        }
+        if (X64 && dirty && (MODE != KBZ_MODE_AFL || simp)) *slot = v;
+      }
+      // column ORs of this wave's words: lane wi holds word wi's OR
+      const bool mine = lane < TW / 8 && ((lane >> 1) % NX) == xi;
+      if (mine) {
+#pragma unroll
+        for (int k = 0; k < NC; k++)
+          if (present[k]) {
+            const size_t off = (size_t)k * a.map_size + (size_t)t * TW + (size_t)lane * 8;
+            *(uint64_t *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) = orw[k];
+            if (orw[k])
+              atomicOr((unsigned long long *)(a.segor + (size_t)seg * NC * a.map_size + off),
+                       (unsigned long long)orw[k]);
+          }
+      }
+    };
+    for (uint32_t g = 0; g < nsteps; g += D) {
+      for (int u = 0; u < D; u++) {
+        const uint32_t s = g + u;
+        if (s >= 1 && s - 1 < ntiles) transform_tile(s - 1);
+        lds_barrier();
+      }
+    }
+    neqs[xi][lane] = neq;
+    lds_barrier();  // (Z)
   }
 }
 
@@ -947,6 +1173,11 @@ void free_ctx(kbz_ctx *c) {
   delete c;
 }
 
+#ifndef KBZ_WIDE_NX
+#define KBZ_WIDE_NX 4
+#endif
+constexpr int kWideNX = KBZ_WIDE_NX;        // transform waves of k_pass1w
+constexpr uint32_t kWideBelowChunks = 512;  // 2 chunks per CU on a 256-CU MI355X
 #ifndef KBZ_PASS1_DEPTH
 #define KBZ_PASS1_DEPTH 2
 #endif
@@ -970,7 +1201,16 @@ void launch_pass1(const Pass1Args &a, uint32_t chunks, hipStream_t s) {
   if (abl == 3) return launch_abl<MODE, IGN, X64, 3>(depth, a, chunks, s);
   return launch_abl<MODE, IGN, X64, 0>(depth, a, chunks, s);
 #else
-  hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, 0, KBZ_PASS1_DEPTH>), dim3(chunks), dim3(128), 0, s, a);
+  // Fewer chunks than two per CU (large maps, small batches): the wide-map variant.
+  // KBZ_PASS1=narrow|wide overrides the choice (A/B timing).
+  static const char *force = getenv("KBZ_PASS1");
+  const bool wide = force ? !strcmp(force, "wide") : chunks < kWideBelowChunks;
+  if (wide)
+    hipLaunchKernelGGL((k_pass1w<MODE, IGN, X64, kWideNX>), dim3(chunks), dim3(64 * (2 + kWideNX)),
+                       0, s, a);
+  else
+    hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, 0, KBZ_PASS1_DEPTH>), dim3(chunks), dim3(128), 0,
+                       s, a);
 #endif
 }
 
