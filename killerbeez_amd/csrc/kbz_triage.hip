@@ -116,12 +116,31 @@ __device__ __forceinline__ void vmcnt_wait() {
 // The same wait naming the ring slot's registers "+v" (cdna_hip_programming.md, asm loads form
 // (ii)): no consumer of them, a register copy included, is scheduled above it.
 template <int N>
+__device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[4]) {
+  asm volatile("s_waitcnt vmcnt(%4)"
+               : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3])
+               : "n"(N)
+               : "memory");
+}
+template <int N>
 __device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[8]) {
   asm volatile("s_waitcnt vmcnt(%8)"
                : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
                  "+v"(r[6]), "+v"(r[7])
                : "n"(N)
                : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[9]) {
+  asm volatile("s_waitcnt vmcnt(%9)"
+               : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
+                 "+v"(r[6]), "+v"(r[7]), "+v"(r[8])
+               : "n"(N)
+               : "memory");
+}
+// cached (not nontemporal) 16-B load: data every workgroup re-reads (the virgin maps)
+__device__ __forceinline__ void asm_load16_cached(u32x4 &r, const uint8_t *p) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
 }
 // Drain every asm load, keeping their destination registers live up to the wait: an asm
 // load's output looks ready to the compiler, so once it is dead the compiler may reuse the
@@ -195,6 +214,9 @@ struct Pass1Args {
   uint32_t *shard_last; // [2]
   uint8_t *segor;       // [nseg][nclass][map_size], zero on entry: OR'ed into with atomics
   uint32_t seg_len;     // chunks per segment
+  const uint8_t *vcur;  // [3][map_size] virgin maps at batch entry
+  uint64_t *tflags;     // [chunks][nclass][nfw]: bit t%64 of word t/64 = tile t of chunk_or stored
+  uint32_t nfw;         // flag words per (chunk, class) = ceil(tiles / 64)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -225,8 +247,8 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = 8;  // 8 x 1-KiB loads per wave per tile
   constexpr int TILE = kChunk * SLOTS;                     // uint4 per tile buffer
-  // 2 tile buffers (32 KiB) + 8 KiB pad: at most 4 chunks per CU, so 1,024 chunks spread
-  // over all 256 CUs
+  // 2 tile buffers (32 KiB) + 8 KiB: wave T's virgin words (2 x 768 B) and padding, at most 4
+  // chunks per CU, so 1,024 chunks spread over all 256 CUs
   __shared__ uint4 lds[2 * TILE + 512];
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -267,11 +289,10 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
       lds[b * TILE + rr * SLOTS + (ls ^ (rr & 15))] = make_uint4(v.x, v.y, v.z, v.w);
     }
   };
-  u32x4 R[D][NLD];
-#pragma unroll
-  for (int d = 0; d < D; d++) load_half(R[d], d);
-
   if (wave == 0) {
+    u32x4 R[D][NLD];
+#pragma unroll
+    for (int d = 0; d < D; d++) load_half(R[d], d);
     // ------------------------------------------------------------------ wave L
     uint64_t h = (uint64_t)(kHashConst ^ a.map_size);
     uint64_t x0 = kXP1 + kXP2, x1 = kXP2, x2 = 0, x3 = 0 - kXP1;
@@ -374,6 +395,30 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
     }
     uint64_t neq = 0;
     const uint32_t seg = chunk / a.seg_len;
+    // Virgin words of each tile travel with its rows: a 9th ring register per slot (lane l < 16 NC
+    // loads 16 B of class l / 16), stored to a per-buffer LDS area next to the tile, so T can
+    // limit its stores to words that still hold virgin bits (below).
+    u32x4 R[D][NLD + 1];
+    const uint32_t vl = min(lane, 16 * NC - 1);
+    const uint8_t *vbase = a.vcur + (size_t)(vl / 16) * a.map_size + (vl % 16) * 16;
+    auto load_t = [&](u32x4 (&r)[NLD + 1], uint32_t t) {
+      load_half(*(u32x4(*)[NLD])r, t);
+      const uint32_t msk = t < ntiles ? ~0u : 0u;
+      asm_load16_cached(r[NLD], vbase + ((t * TW) & msk));
+    };
+    auto store_t = [&](const u32x4 (&r)[NLD + 1], int b) {
+      store_half(*(const u32x4(*)[NLD])r, b);
+      if (lane < 16 * NC) {
+        const u32x4 v = r[NLD];
+        lds[2 * TILE + b * 48 + lane] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+    };
+#pragma unroll
+    for (int d = 0; d < D; d++) load_t(R[d], d);
+    uint64_t tfl[NC];  // stored-tile bits of the current 64-tile flag word
+#pragma unroll
+    for (int k = 0; k < NC; k++) tfl[k] = 0;
+    uint64_t *tfbase = a.tflags + (size_t)chunk * NC * a.nfw;
     auto transform_tile = [&](uint32_t s) {
       const int b = s & 1;
       const uint64_t *ig = IGN ? (const uint64_t *)(a.ignore + (size_t)s * TW) : nullptr;
@@ -418,31 +463,48 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         // raw AFL words are their own transform (only simplified lanes change)
         if (dirty && (MODE != KBZ_MODE_AFL || simp)) *slot = v;
       }
-      if (lane < TW / 8) {
+      // chunk_or keeps only bits still virgin at batch entry (orw & V): the scan uses nothing
+      // else (its new bits are o & V & ~prev, and f2 only looks at bytes with V == 0xff), and a
+      // tile with none is not stored at all, only its flag bit stays clear.  In steady-state
+      // fuzzing almost no tile is stored, which keeps these stores (and the drain of the
+      // prefetch they cause: vmcnt counts them) off the stream.
 #pragma unroll
-        for (int k = 0; k < NC; k++)
-          if (present[k]) {
-            const size_t off = (size_t)k * a.map_size + (size_t)s * TW + (size_t)lane * 8;
-            *(uint64_t *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) = orw[k];
-            // segment aggregate: most words are 0 (no atomic); hot words collide seg_len-way
-            if (orw[k])
-              atomicOr((unsigned long long *)(a.segor + (size_t)seg * NC * a.map_size + off),
-                       (unsigned long long)orw[k]);
-          }
+      for (int k = 0; k < NC; k++) {
+        if (!present[k]) continue;
+        const size_t off = (size_t)k * a.map_size + (size_t)s * TW + (size_t)lane * 8;
+        const uint64_t m = orw[k] & ((const uint64_t *)&lds[2 * TILE + b * 48 + k * 16])[lane & 31];
+        if (__ballot(lane < TW / 8 && m != 0)) {
+          tfl[k] |= 1ull << (s & 63);
+#ifndef KBZ_XP_NOCOR
+          if (lane < TW / 8) *(uint64_t *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) = m;
+#endif
+        }
+        // segment aggregate: most words are 0 (no atomic); hot words collide seg_len-way
+#ifdef KBZ_XP_NOATOMIC
+        if (false)
+#else
+        if (lane < TW / 8 && orw[k])
+#endif
+          atomicOr((unsigned long long *)(a.segor + (size_t)seg * NC * a.map_size + off),
+                   (unsigned long long)orw[k]);
+        if ((s & 63) == 63 || s + 1 == ntiles) {
+          if (lane == 0) tfbase[k * a.nfw + (s >> 6)] = tfl[k];
+          tfl[k] = 0;
+        }
       }
     };
     lds_barrier();  // (A): L's half of tile 0 is in buffer 0
     KBZ_STAMP_DECL;
     // step s: store own half of tile s (ring slot s%D), prefetch tile s+D into that slot,
-    // transform tile s.
+    // transform tile s.  T issues NLD + NC loads per step.
     for (uint32_t g = 0; g <= ntiles; g += D) {
 #pragma unroll
       for (int u = 0; u < D; u++) {
         const uint32_t s = g + u;
-        vmcnt_wait<(D - 1) * NLD>();
+        vmcnt_wait_ring<(D - 1) * (NLD + 1)>(R[u]);
         KBZ_STAMP(1);
-        store_half(R[u], s & 1);
-        load_half(R[u], s + D);
+        store_t(R[u], s & 1);
+        load_t(R[u], s + D);
         KBZ_STAMP(2);
         if (s < ntiles) transform_tile(s);
         KBZ_STAMP(0);
@@ -462,9 +524,10 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
 // compute-bound twice over (MI355X, config 3: 27.2 ms per batch; 9.3 ms without the transform
 // work, 3.3 ms with neither transform nor chains).  Here the per-word work is spread over
 // NX transform waves and the serial chain is cut to its dependent part:
-//   wave L:      loads rows 0-31 of tile s, and chains tile s-2: per word only the
-//                hash32 step (xor, rotl, *5+C) on the mixed word X computed (+ XXH64 rounds);
-//   wave F:      loads rows 32-63 of tile s (no compute);
+//   waves 0..NL-1 load 64/NL rows each of tile s into a DW-deep register ring (one workgroup
+//                per CU needs ~128 KiB in flight per CU: NL=4 x DW=8 x 4 KiB); wave 0 (L) also
+//                chains tile s-2: per word only the hash32 step (xor, rotl, *5+C) on the mixed
+//                word the X waves computed (+ XXH64 rounds);
 //   waves X_i:   transform tile s-1 (words of slots q with q % NX == i): classify / simplify in
 //                place, column ORs over the 64 traces (DPP), DynamoRIO neighbour equality, and
 //                the per-word hash32 mix k = h32_mix(word & ignore) into the k buffer; they store
@@ -473,13 +536,14 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
 // A tile lives in buffer s % 3 for three steps (filled, transformed, chained); its k values in
 // kbuf[s % 3], stored [slot][row][2] so both the writes (lane = row) and L's row-per-lane
 // ds_read_b128 are conflict-free.  Steps s = 0..ntiles+1, rounded up to a multiple of D, one
-// barrier each.  Same vmcnt accounting as k_pass1s for L and F (only their NLD loads per step).
-// LDS 98 KiB: one workgroup per CU, 2+NX waves.
+// barrier each.  Same vmcnt accounting as k_pass1s for the loaders (only their loads per step).
+// LDS 98 KiB: one workgroup per CU, NL+NX waves.
 // ---------------------------------------------------------------------------------------------
-template <int MODE, bool IGN, bool X64, int NX, int D = 2>
-__global__ __launch_bounds__(64 * (2 + NX), 1) void k_pass1w(Pass1Args a) {
+template <int MODE, bool IGN, bool X64, int NX, int NL, int D>
+__global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
+  static_assert(NL == 2 || NL == 4, "64/NL rows per loader, 4 rows per wave-load");
   constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
-  constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = 8;
+  constexpr int TW = 256, SLOTS = 16, RPI = 4, RPW = kChunk / NL, NLD = RPW / RPI;
   constexpr int TILE = kChunk * SLOTS;  // uint4 per tile buffer
   __shared__ uint4 lds[3 * TILE];
   __shared__ uint4 kbuf[3 * TILE];      // [buf][slot][row] of {k(2q), k(2q+1)}
@@ -497,14 +561,14 @@ __global__ __launch_bounds__(64 * (2 + NX), 1) void k_pass1w(Pass1Args a) {
   const uint32_t ntiles = a.map_size / TW;
   const uint32_t nsteps = ntiles + 2;
 
-  if (wave < 2) {
-    // ------------------------------------------------------------ waves L (0) and F (1)
+  if (wave < NL) {
+    // ------------------------------------------------------------ loader waves (0 = L)
     const int lr = lane / SLOTS, ls = lane % SLOTS;
     const uint8_t *lbase = a.traces + row0 * a.stride + ls * 16;
     uint32_t roff[NLD];
 #pragma unroll
     for (int i = 0; i < NLD; i++)
-      roff[i] = (uint32_t)(min(32 * wave + RPI * i + lr, nrows - 1) * a.stride);
+      roff[i] = (uint32_t)(min(RPW * wave + RPI * i + lr, nrows - 1) * a.stride);
     auto load_half = [&](u32x4 (&r)[NLD], uint32_t t) {  // branch-free (see k_pass1s)
       const uint32_t msk = t < ntiles ? ~0u : 0u;
 #pragma unroll
@@ -513,7 +577,7 @@ __global__ __launch_bounds__(64 * (2 + NX), 1) void k_pass1w(Pass1Args a) {
     auto store_half = [&](const u32x4 (&r)[NLD], int b) {
 #pragma unroll
       for (int i = 0; i < NLD; i++) {
-        const int rr = 32 * wave + RPI * i + lr;
+        const int rr = RPW * wave + RPI * i + lr;
         const u32x4 v = r[i];
         lds[b * TILE + rr * SLOTS + (ls ^ (rr & 15))] = make_uint4(v.x, v.y, v.z, v.w);
       }
@@ -586,10 +650,12 @@ __global__ __launch_bounds__(64 * (2 + NX), 1) void k_pass1w(Pass1Args a) {
     }
   } else {
     // ------------------------------------------------------------ waves X_i
-    const int xi = wave - 2;
+    const int xi = wave - NL;
     uint64_t present[NC];
 #pragma unroll
     for (int k = 0; k < NC; k++) present[k] = __ballot(valid && cls == k);
+    if (xi == 0)  // every tile of chunk_or is stored (unmasked) here: all flags set
+      for (uint32_t i = lane; i < NC * a.nfw; i += 64) a.tflags[(size_t)chunk * NC * a.nfw + i] = ~0ull;
     if (xi == 0 && lane == 0) {
       uint8_t m = 0;
 #pragma unroll
@@ -709,7 +775,17 @@ struct FixArgs {
   uint8_t *chunk_or;
   const uint8_t *chunk_cls;
   uint32_t nchunks, seg_len;
+  const uint32_t *listed;  // [chunks] nonzero: in fix_list
+  const uint64_t *tflags;  // pass 1's stored-tile bits (class 0), see Pass1Args
+  uint32_t nfw;
 };
+// Was tile col/256 of chunk c's class-k row of chunk_or stored by pass 1?  An unstored tile
+// held no still-virgin bit: it reads as 0.
+__device__ __forceinline__ bool tile_stored(const uint64_t *tflags, uint32_t nfw, int nclass,
+                                            uint32_t c, int k, uint32_t col) {
+  const uint32_t t = col / kTileW;
+  return (tflags[((size_t)c * nclass + k) * nfw + (t >> 6)] >> (t & 63)) & 1;
+}
 __device__ void fix_column(const FixArgs &f, uint32_t map_size, uint32_t col, uint8_t *segor) {
   const uint32_t cnt = *f.fix_cnt;
   for (uint32_t i = 0; i < cnt; i++) {
@@ -726,7 +802,8 @@ __device__ void fix_column(const FixArgs &f, uint32_t map_size, uint32_t col, ui
     const uint32_t c0 = seg * f.seg_len, c1 = min(f.nchunks, c0 + f.seg_len);
     uint64_t acc = 0;
     for (uint32_t c = c0; c < c1; c++)
-      if (f.chunk_cls[c] & 1) acc |= *(const uint64_t *)(f.chunk_or + (size_t)c * map_size + col);
+      if ((f.chunk_cls[c] & 1) && (f.listed[c] || tile_stored(f.tflags, f.nfw, 1, c, 0, col)))
+        acc |= *(const uint64_t *)(f.chunk_or + (size_t)c * map_size + col);
     *(uint64_t *)(segor + (size_t)seg * map_size + col) = acc;
   }
 }
@@ -818,7 +895,9 @@ __global__ __launch_bounds__(256) void k_scan(const uint8_t *chunk_or, const uin
                                                const uint8_t *gprefix, const uint8_t *gtotal,
                                                const uint8_t *vcur, uint8_t *vnext,
                                                const uint8_t *ignore, uint64_t *items,
-                                               uint32_t cap, uint32_t *counters) {
+                                               uint32_t cap, uint32_t *counters,
+                                               const uint64_t *tflags, uint32_t nfw,
+                                               const uint32_t *listed) {
   // no per-lane early return: every lane of a wave takes part in the item-allocation prefix
   const uint32_t col0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
   const bool live = col0 < map_size;
@@ -857,16 +936,20 @@ __global__ __launch_bounds__(256) void k_scan(const uint8_t *chunk_or, const uin
   // stale row: masked to 0 after the load) so each batch costs one memory round trip
   for (uint32_t cb = c0; cb < c1; cb += 8) {
     uint4 o[8];
+    bool st[8];
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       const uint32_t c = min(cb + u, c1 - 1);
       o[u] = *(const uint4 *)(chunk_or + (size_t)c * nclass * map_size + kc);
+      // DynamoRIO fix path: a listed chunk's row was rewritten whole (unmasked) by k_total
+      st[u] = tile_stored(tflags, nfw, nclass, c, k, col) || (listed && listed[c]);
     }
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       const uint32_t c = cb + u;  // uniform across the block
       if (c >= c1) break;
       if (!((chunk_cls[c] >> k) & 1)) continue;
+      if (!st[u]) o[u] = make_uint4(0, 0, 0, 0);  // nothing still virgin in that tile
       const uint4 nb = make_uint4(o[u].x & vr.x & ~prev.x, o[u].y & vr.y & ~prev.y,
                                   o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
       if (__ballot(nb.x | nb.y | nb.z | nb.w))  // wave-uniform: all lanes join the prefix
@@ -1082,6 +1165,8 @@ struct kbz_ctx {
   uint8_t *ignore = nullptr;
   uint8_t *chunk_or = nullptr;
   uint8_t *chunk_cls = nullptr;
+  uint64_t *tflags = nullptr;    // [chunks][nc][nfw] stored tiles of chunk_or (Pass1Args)
+  uint32_t nfw = 1;
   uint32_t *flags = nullptr;     // [chunks] queued for recomputation
   uint32_t *fix_list = nullptr;  // [chunks]
   uint8_t *skip = nullptr;
@@ -1156,7 +1241,7 @@ int dalloc(T **p, size_t count) {
 void free_ctx(kbz_ctx *c) {
   if (!c) return;
   DevGuard g(c->device);
-  void *ptrs[] = {c->V[0], c->V[1], c->last, c->ignore, c->chunk_or, c->chunk_cls, c->flags, c->fix_list,
+  void *ptrs[] = {c->V[0], c->V[1], c->last, c->ignore, c->chunk_or, c->chunk_cls, c->tflags, c->flags, c->fix_list,
                   c->skip, c->neq, c->h32, c->hnb32, c->segor, c->segprev, c->total,
                   c->items, c->counters, c->shard_last, c->dslot[0], c->dslot[1],
                   c->dslot_oc[0], c->dslot_oc[1], c->dres_hnb, c->dres_h32, c->dres_x64};
@@ -1174,19 +1259,36 @@ void free_ctx(kbz_ctx *c) {
 }
 
 #ifndef KBZ_WIDE_NX
-#define KBZ_WIDE_NX 4
+#define KBZ_WIDE_NX 12
+#endif
+#ifndef KBZ_WIDE_NL
+#define KBZ_WIDE_NL 2
+#endif
+#ifndef KBZ_WIDE_D
+#define KBZ_WIDE_D 2
 #endif
 constexpr int kWideNX = KBZ_WIDE_NX;        // transform waves of k_pass1w
+constexpr int kWideNL = KBZ_WIDE_NL;        // loader waves of k_pass1w
+constexpr int kWideD = KBZ_WIDE_D;          // their register ring depth
 constexpr uint32_t kWideBelowChunks = 512;  // 2 chunks per CU on a 256-CU MI355X
 #ifndef KBZ_PASS1_DEPTH
 #define KBZ_PASS1_DEPTH 2
 #endif
+// Fewer chunks than two per CU (large maps, small batches): the wide-map variant.
+// KBZ_PASS1=narrow|wide overrides the choice (A/B timing).
+bool pass1_is_wide(uint32_t chunks) {
+#ifdef KBZ_ABLATION
+  return false;
+#else
+  static const char *force = getenv("KBZ_PASS1");
+  return force ? !strcmp(force, "wide") : chunks < kWideBelowChunks;
+#endif
+}
 #ifdef KBZ_ABLATION
 template <int MODE, bool IGN, bool X64, int ABL>
 void launch_abl(int depth, const Pass1Args &a, uint32_t chunks, hipStream_t s) {
   if (depth == 2) hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, ABL, 2>), dim3(chunks), dim3(128), 0, s, a);
   else if (depth == 3) hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, ABL, 3>), dim3(chunks), dim3(128), 0, s, a);
-  else if (depth == 6) hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, ABL, 6>), dim3(chunks), dim3(128), 0, s, a);
   else hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, ABL, 4>), dim3(chunks), dim3(128), 0, s, a);
 }
 #endif
@@ -1201,13 +1303,9 @@ void launch_pass1(const Pass1Args &a, uint32_t chunks, hipStream_t s) {
   if (abl == 3) return launch_abl<MODE, IGN, X64, 3>(depth, a, chunks, s);
   return launch_abl<MODE, IGN, X64, 0>(depth, a, chunks, s);
 #else
-  // Fewer chunks than two per CU (large maps, small batches): the wide-map variant.
-  // KBZ_PASS1=narrow|wide overrides the choice (A/B timing).
-  static const char *force = getenv("KBZ_PASS1");
-  const bool wide = force ? !strcmp(force, "wide") : chunks < kWideBelowChunks;
-  if (wide)
-    hipLaunchKernelGGL((k_pass1w<MODE, IGN, X64, kWideNX>), dim3(chunks), dim3(64 * (2 + kWideNX)),
-                       0, s, a);
+  if (pass1_is_wide(chunks))
+    hipLaunchKernelGGL((k_pass1w<MODE, IGN, X64, kWideNX, kWideNL, kWideD>), dim3(chunks),
+                       dim3(64 * (kWideNL + kWideNX)), 0, s, a);
   else
     hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, 0, KBZ_PASS1_DEPTH>), dim3(chunks), dim3(128), 0,
                        s, a);
@@ -1271,10 +1369,12 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   c->nc = mode_nclass(mode);
   c->max_batch = max_batch;
   c->max_chunks = cdiv(max_batch, kChunk);
+  c->nfw = cdiv(map_size / kTileW, 64);
   const size_t M = map_size, nc = c->nc;
   c->item_cap = (uint32_t)std::min<size_t>(kItemsPerCol * M * nc + 1024, 0xffffffffu);
   bool ok = !dalloc(&c->V[0], 3 * M) && !dalloc(&c->V[1], 3 * M) && !dalloc(&c->last, 2) &&
             !dalloc(&c->chunk_or, c->max_chunks * nc * M) && !dalloc(&c->chunk_cls, c->max_chunks) &&
+            !dalloc(&c->tflags, c->max_chunks * nc * c->nfw) &&
             !dalloc(&c->flags, c->max_chunks) && !dalloc(&c->fix_list, c->max_chunks) &&
             !dalloc(&c->skip, max_batch) &&
             !dalloc(&c->neq, max_batch) && !dalloc(&c->h32, max_batch) &&
@@ -1389,6 +1489,9 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
   a.shard_last = c->shard_last;
   a.segor = c->segor;
   a.seg_len = c->cur_seg_len;
+  a.vcur = c->V[c->vcur];
+  a.tflags = c->tflags;
+  a.nfw = c->nfw;
   if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, s)) return -1;
   c->stage = 1;
   return 0;
@@ -1443,6 +1546,9 @@ int kbz_shard_reduce(kbz_ctx_t *c, void *stream) {
       fx.chunk_cls = c->chunk_cls;
       fx.nchunks = c->cur_chunks;
       fx.seg_len = c->cur_seg_len;
+      fx.listed = c->flags;
+      fx.tflags = c->tflags;
+      fx.nfw = c->nfw;
     }
     hipLaunchKernelGGL(k_total, dim3(cdiv(c->M / 8, 256), 1, c->nc), dim3(256), 0, s, c->segor,
                        c->cur_nseg, c->nc, (uint32_t)c->M, c->segprev, c->total, fx);
@@ -1475,7 +1581,8 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
   hipLaunchKernelGGL(k_scan, dim3(gx, nseg, c->nc), dim3(256), 0, s, c->chunk_or, c->chunk_cls,
                      c->cur_chunks, c->cur_seg_len, c->nc, (uint32_t)c->M, c->segprev, nseg,
                      c->total, prefix, total, c->V[c->vcur], c->V[vn], ign, c->items,
-                     c->item_cap, c->counters);
+                     c->item_cap, c->counters, c->tflags, c->nfw,
+                     c->mode == KBZ_MODE_DYNAMORIO ? c->flags : nullptr);
   HIP_TRY(hipGetLastError());
   if (c->cur_n) {
     hipLaunchKernelGGL(k_resolve, dim3(512), dim3(256), 0, s, c->cur_traces, c->cur_stride,
