@@ -132,7 +132,9 @@ int kbz_shard_link(kbz_ctx_t *ctx, const uint32_t *prev_last, int is_first,
                    const uint32_t *global_last, void *stream);
 int kbz_shard_reduce(kbz_ctx_t *ctx, void *stream);
 /* Copies this shard's OR aggregate (nclass*map_size bytes; nclass = 1 in DYNAMORIO mode,
- * 3 otherwise) into device memory d_out. */
+ * 3 otherwise) into device memory d_out.  Only bits still virgin at batch entry are kept (the
+ * OR of the transformed traces & V): all ranks hold the same V, and the protocol uses the
+ * aggregates only under & V. */
 int kbz_shard_aggregate(kbz_ctx_t *ctx, uint8_t *d_out, void *stream);
 size_t kbz_shard_aggregate_bytes(kbz_ctx_t *ctx);
 /* prefix/total: device, nclass*map_size bytes each (prefix may be NULL = all zero; total may be

@@ -475,18 +475,13 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         const uint64_t m = orw[k] & ((const uint64_t *)&lds[2 * TILE + b * 48 + k * 16])[lane & 31];
         if (__ballot(lane < TW / 8 && m != 0)) {
           tfl[k] |= 1ull << (s & 63);
-#ifndef KBZ_XP_NOCOR
           if (lane < TW / 8) *(uint64_t *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) = m;
-#endif
         }
-        // segment aggregate: most words are 0 (no atomic); hot words collide seg_len-way
-#ifdef KBZ_XP_NOATOMIC
-        if (false)
-#else
-        if (lane < TW / 8 && orw[k])
-#endif
+        // segment aggregate, restricted to still-virgin bits like chunk_or (its consumers only
+        // use it under & V: k_scan's segment test and V' = V & ~total): almost never an atomic
+        if (lane < TW / 8 && m)
           atomicOr((unsigned long long *)(a.segor + (size_t)seg * NC * a.map_size + off),
-                   (unsigned long long)orw[k]);
+                   (unsigned long long)m);
         if ((s & 63) == 63 || s + 1 == ntiles) {
           if (lane == 0) tfbase[k * a.nfw + (s >> 6)] = tfl[k];
           tfl[k] = 0;

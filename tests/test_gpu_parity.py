@@ -249,3 +249,77 @@ def test_full_size_config2(gpu):
     torch.cuda.synchronize()
     assert int(out2["hnb"].max()) == 0
     np.testing.assert_array_equal(ctx.get_virgin(), v)
+
+
+def _run_shards(ctxs, shards, ocs, mode, device):
+    """One sharded batch over in-process 'ranks' (one context each, same GPU), phase by phase
+    as killerbeez_amd.dist.triage_sharded runs them, with the all-gathers done locally."""
+    import torch
+
+    world = len(ctxs)
+    counts = [s.shape[0] for s in shards]
+    outs = [c.shard_begin(s, o, WANT_H32) for c, s, o in zip(ctxs, shards, ocs)]
+    nonempty = [r for r in range(world) if counts[r] > 0]
+    if mode == MODE_DYNAMORIO:
+        pairs = torch.stack([c.shard_last_hash(torch.empty(2, dtype=torch.int32, device=device))
+                             for c in ctxs])
+        for r, c in enumerate(ctxs):
+            prev = [q for q in nonempty if q < r]
+            c.shard_link(pairs[prev[-1]] if prev else None, not prev,
+                         pairs[nonempty[-1]] if nonempty else None)
+    else:
+        for c in ctxs:
+            c.shard_link(None, True, None)
+    for c in ctxs:
+        c.shard_reduce()
+    nb = ctxs[0].shard_aggregate_bytes()
+    allagg = torch.stack([c.shard_aggregate(torch.empty(nb, dtype=torch.uint8, device=device))
+                          for c in ctxs])
+    total = torch.empty(nb, dtype=torch.uint8, device=device)
+    TriageContext.or_reduce(total, allagg, 0, world, nb)
+    res = []
+    for r, c in enumerate(ctxs):
+        prefix = None
+        if r > 0:
+            prefix = torch.empty(nb, dtype=torch.uint8, device=device)
+            TriageContext.or_reduce(prefix, allagg, 0, r, nb)
+        res.append(c.shard_finish(prefix, total))
+    torch.cuda.synchronize()
+    for c in ctxs:
+        c.sync()
+    return (np.concatenate([o["hnb"].cpu().numpy() for o in res]),
+            np.concatenate([o["h32"].cpu().numpy().view(np.uint32) for o in res]))
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("counts", [[700, 324], [640, 0, 193, 64]])
+def test_sharded_protocol_on_gpu(gpu, mode, counts):
+    """The multi-GPU protocol (dist.py) through the C ABI: shard aggregates (restricted to
+    still-virgin bits), prefix/total ORs and the last-hash links give the sequential result,
+    batch after batch (the second batch adds new coverage to carried virgin maps)."""
+    import torch
+
+    m = 4096
+    n = sum(counts)
+    ctxs = [TriageContext(m, mode, max(c, 1)) for c in counts]
+    v = np.full((3, m), 0xFF, np.uint8)
+    last = 0
+    for batch in range(3):
+        t, oc = synth.sparse_np(n, m, seed=100 + batch, hot_frac=0.05)
+        t[300] = t[299]          # DynamoRIO skips inside and across shards
+        t[counts[0]] = t[counts[0] - 1]
+        exp = oracle.triage_batch(mode, t, oc, virgin=v, last_hash=last, want=oracle.WANT_H32)
+        lo, shards, ocs = 0, [], []
+        for c in counts:
+            shards.append(torch.from_numpy(t[lo:lo + c].copy()).cuda())
+            ocs.append(torch.from_numpy(oc[lo:lo + c].copy()).cuda())
+            lo += c
+        hnb, h32 = _run_shards(ctxs, shards, ocs, mode, torch.device("cuda"))
+        np.testing.assert_array_equal(hnb, exp["hnb"])
+        np.testing.assert_array_equal(h32, exp["h32"])
+        for c in ctxs:
+            np.testing.assert_array_equal(c.get_virgin(), exp["virgin"])
+            if mode == MODE_DYNAMORIO:
+                assert c.last_hash == exp["last_hash"]
+        v, last = exp["virgin"], exp.get("last_hash", 0)
+        assert batch == 0 or 0 < (hnb > 0).sum() < n  # later batches still find something
