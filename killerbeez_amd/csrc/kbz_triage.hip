@@ -519,30 +519,38 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
 // compute-bound twice over (MI355X, config 3: 27.2 ms per batch; 9.3 ms without the transform
 // work, 3.3 ms with neither transform nor chains).  Here the per-word work is spread over
 // NX transform waves and the serial chain is cut to its dependent part:
-//   waves 0..NL-1 load 64/NL rows each of tile s into a DW-deep register ring (one workgroup
-//                per CU needs ~128 KiB in flight per CU: NL=4 x DW=8 x 4 KiB); wave 0 (L) also
+//   waves 0..NL-1 load 64/NL rows each of tile s into a D-deep register ring; wave 0 (L) also
 //                chains tile s-2: per word only the hash32 step (xor, rotl, *5+C) on the mixed
 //                word the X waves computed (+ XXH64 rounds);
-//   waves X_i:   transform tile s-1 (words of slots q with q % NX == i): classify / simplify in
-//                place, column ORs over the 64 traces (DPP), DynamoRIO neighbour equality, and
-//                the per-word hash32 mix k = h32_mix(word & ignore) into the k buffer; they store
-//                their words' column ORs and segment atomics (X waves issue no asm loads, so
-//                their stores disturb no counted wait).
+//   waves X_i:   transform tile s-1 COLUMN-wise: lane (w = lane % 32, half h = lane / 32) owns
+//                word w of the rows of row group g = 2 i + h (64 / (2 NX) consecutive rows).
+//                Per (row, word): classify / simplify (written back in place for XXH64), the
+//                hash32 mix k = h32_mix(word & ignore) into the k buffer, a plain per-lane OR
+//                per class, and the DynamoRIO neighbour test against the previous row of the
+//                same lane (a ballot per row; group boundaries are compared one step later
+//                through LDS).  The groups' ORs meet in LDS (ds_or_b64); X_0 stores them
+//                (chunk_or, segment atomics) one step later.  X waves issue no asm loads, so
+//                their stores disturb no counted wait.
 // A tile lives in buffer s % 3 for three steps (filled, transformed, chained); its k values in
-// kbuf[s % 3], stored [slot][row][2] so both the writes (lane = row) and L's row-per-lane
-// ds_read_b128 are conflict-free.  Steps s = 0..ntiles+1, rounded up to a multiple of D, one
-// barrier each.  Same vmcnt accounting as k_pass1s for the loaders (only their loads per step).
-// LDS 98 KiB: one workgroup per CU, NL+NX waves.
+// kbuf[s % 3] with the tile's own swizzled [row][slot] layout, so the X writes (32 lanes per
+// row) and L's row-per-lane ds_read_b128 are both conflict-free.  Steps s = 0..ntiles+1,
+// rounded up to a multiple of D, one barrier each.  Same vmcnt accounting as k_pass1s for the
+// loaders (only their loads per step).  LDS ~106 KiB: one workgroup per CU, NL+NX waves.
 // ---------------------------------------------------------------------------------------------
-template <int MODE, bool IGN, bool X64, int NX, int NL, int D>
-__global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
+template <int MODE, bool IGN, bool X64, int NX, int NL, int D, bool ISO>
+__global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a) {
   static_assert(NL == 2 || NL == 4, "64/NL rows per loader, 4 rows per wave-load");
+  static_assert(!ISO || (NL == 2 && NX == 8), "ISO layout: 11 waves");
+  static_assert(kChunk % (2 * NX) == 0, "equal row groups");
   constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, RPW = kChunk / NL, NLD = RPW / RPI;
   constexpr int TILE = kChunk * SLOTS;  // uint4 per tile buffer
+  constexpr int RG = kChunk / (2 * NX);  // rows per X row group
   __shared__ uint4 lds[3 * TILE];
-  __shared__ uint4 kbuf[3 * TILE];      // [buf][slot][row] of {k(2q), k(2q+1)}
-  __shared__ uint64_t neqs[NX][kChunk];
+  __shared__ uint4 kbuf[3 * TILE];             // k of each (row, word), same layout as lds
+  __shared__ uint64_t orb[3][NC][TW / 8];      // column ORs of the tile, per class
+  __shared__ uint64_t bnd[2][2 * NX][TW / 8];  // last row of each group (neighbour test)
+  __shared__ uint64_t neqs[NX];
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const uint32_t chunk = blockIdx.x;
@@ -551,19 +559,25 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
   const bool valid = lane < nrows;
   const int oc = (valid && a.outcome) ? a.outcome[row0 + lane] : KBZ_FUZZ_NONE;
   const int cls = class_of(MODE, oc);
-  const int xf = valid ? class_xf(MODE, cls) : XF_RAW;
-  const bool simp = (xf == XF_SIMPLIFY);
   const uint32_t ntiles = a.map_size / TW;
   const uint32_t nsteps = ntiles + 2;
 
-  if (wave < NL) {
-    // ------------------------------------------------------------ loader waves (0 = L)
+  // Roles.  Default: waves 0..NL-1 load, wave 0 (L) also chains, the rest transform.  ISO (11
+  // waves, dispatched round-robin over the 4 SIMDs): L = wave 0 only chains, the loaders are
+  // waves 4 and 8, so L's SIMD runs no transform work (the chain is latency-bound and is the
+  // critical path of this kernel); X waves are 1-3, 5-7, 9-10.
+  const bool isL = wave == 0;
+  const bool isLd = ISO ? (wave == 4 || wave == 8) : wave < NL;
+  const int li = ISO ? (wave >> 3) : wave;
+  const int xrole = ISO ? wave - 1 - (wave > 4) - (wave > 8) : wave - NL;
+  if (isL || isLd) {
+    // ------------------------------------------------------------ loader waves and L
     const int lr = lane / SLOTS, ls = lane % SLOTS;
     const uint8_t *lbase = a.traces + row0 * a.stride + ls * 16;
     uint32_t roff[NLD];
 #pragma unroll
     for (int i = 0; i < NLD; i++)
-      roff[i] = (uint32_t)(min(RPW * wave + RPI * i + lr, nrows - 1) * a.stride);
+      roff[i] = (uint32_t)(min(RPW * li + RPI * i + lr, nrows - 1) * a.stride);
     auto load_half = [&](u32x4 (&r)[NLD], uint32_t t) {  // branch-free (see k_pass1s)
       const uint32_t msk = t < ntiles ? ~0u : 0u;
 #pragma unroll
@@ -572,7 +586,7 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
     auto store_half = [&](const u32x4 (&r)[NLD], int b) {
 #pragma unroll
       for (int i = 0; i < NLD; i++) {
-        const int rr = RPW * wave + RPI * i + lr;
+        const int rr = RPW * li + RPI * i + lr;
         const u32x4 v = r[i];
         lds[b * TILE + rr * SLOTS + (ls ^ (rr & 15))] = make_uint4(v.x, v.y, v.z, v.w);
       }
@@ -581,20 +595,19 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
     uint64_t x0 = kXP1 + kXP2, x1 = kXP2, x2 = 0, x3 = 0 - kXP1;
     auto chain_tile = [&](uint32_t t) {
       const int b = t % 3;
-      const uint4 *krow = &kbuf[b * TILE + lane];
+      const uint4 *krow = &kbuf[b * TILE + lane * SLOTS];
       const uint4 *row = &lds[b * TILE + lane * SLOTS];
       const int sw = lane & 15;
 #pragma unroll 4
       for (int q = 0; q < SLOTS; q++) {
-        const uint4 kk = krow[q * kChunk];
+        const uint4 kk = krow[q ^ sw];
         h = h32_step_fast(h, (uint64_t)kk.x | ((uint64_t)kk.y << 32));
         h = h32_step_fast(h, (uint64_t)kk.z | ((uint64_t)kk.w << 32));
         if (X64) {
-          const uint4 v = row[q ^ sw];
+          const uint4 v = row[q ^ sw];  // transformed in place by the X waves
 #pragma unroll
           for (int e = 0; e < 2; e++) {
-            uint64_t tw = ld_u64(v, e);
-            if (simp && tw == 0) tw = kSimpleZero;  // an untransformed zero word (see k_pass1s)
+            const uint64_t tw = ld_u64(v, e);
             const int xl = (2 * q + e) & 3;
             if (xl == 0) x0 = xx_round(x0, tw);
             else if (xl == 1) x1 = xx_round(x1, tw);
@@ -604,23 +617,36 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
         }
       }
     };
-    u32x4 R[D][NLD];
+    if (isLd) {  // the whole ring lives inside this wave-uniform branch
+      u32x4 R[D][NLD];
 #pragma unroll
-    for (int d = 0; d < D; d++) load_half(R[d], d);
-    for (uint32_t g = 0; g < nsteps; g += D) {
+      for (int d = 0; d < D; d++) load_half(R[d], d);
+      for (uint32_t g = 0; g < nsteps; g += D) {
 #pragma unroll
-      for (int u = 0; u < D; u++) {
-        const uint32_t s = g + u;
-        if (wave == 0 && s >= 2 && s - 2 < ntiles) chain_tile(s - 2);
-        vmcnt_wait_ring<(D - 1) * NLD>(R[u]);
-        store_half(R[u], s % 3);
-        load_half(R[u], s + D);
-        lds_barrier();
+        for (int u = 0; u < D; u++) {
+          const uint32_t s = g + u;
+#ifndef KBZ_XP_NOCHAIN
+          if (isL && s >= 2 && s - 2 < ntiles) chain_tile(s - 2);
+#endif
+          vmcnt_wait_ring<(D - 1) * NLD>(R[u]);
+          store_half(R[u], s % 3);
+          load_half(R[u], s + D);
+          lds_barrier();
+        }
+      }
+      drain_asm_loads(R);
+    } else {  // ISO: L only chains
+      __builtin_amdgcn_s_setprio(3);
+      for (uint32_t g = 0; g < nsteps; g += D) {
+        for (int u = 0; u < D; u++) {
+          const uint32_t s = g + u;
+          if (s >= 2 && s - 2 < ntiles) chain_tile(s - 2);
+          lds_barrier();
+        }
       }
     }
-    drain_asm_loads(R);
     lds_barrier();  // (Z): the X waves' neighbour flags are in neqs
-    if (wave == 0 && valid) {
+    if (isL && valid) {
       const uint32_t h32 = h32_final(h);
       a.h32[row0 + lane] = h32;
       if (X64 && a.x64) {
@@ -637,98 +663,130 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
         a.shard_last[1] = 1;
       }
     }
-    if (wave == 1 && MODE == KBZ_MODE_DYNAMORIO && valid) {
+    if (isLd && li == 1 && MODE == KBZ_MODE_DYNAMORIO && valid) {
       uint64_t nq = 0;
 #pragma unroll
-      for (int i = 0; i < NX; i++) nq |= neqs[i][lane];
-      a.neq[row0 + lane] = nq != 0;
+      for (int i = 0; i < NX; i++) nq |= neqs[i];
+      a.neq[row0 + lane] = (nq >> lane) & 1;
     }
   } else {
-    // ------------------------------------------------------------ waves X_i
-    const int xi = wave - NL;
+    // ------------------------------------------------------------ waves X_i (column-wise)
+    const int xi = xrole;
+    const int w = lane & 31, hf = lane >> 5;
+    const int grp = 2 * xi + hf;
+    const int r0 = grp * RG;             // this lane's rows: r0 .. r0 + RG - 1
+    const int r0a = 2 * xi * RG, r0b = r0a + RG;  // first rows of the wave's two groups
     uint64_t present[NC];
 #pragma unroll
     for (int k = 0; k < NC; k++) present[k] = __ballot(valid && cls == k);
-    if (xi == 0)  // every tile of chunk_or is stored (unmasked) here: all flags set
-      for (uint32_t i = lane; i < NC * a.nfw; i += 64) a.tflags[(size_t)chunk * NC * a.nfw + i] = ~0ull;
-    if (xi == 0 && lane == 0) {
-      uint8_t m = 0;
+    // 2-bit class code of each of this lane's rows (3: past the end of a partial chunk)
+    uint32_t clsw = 0;
 #pragma unroll
-      for (int k = 0; k < NC; k++) m |= present[k] ? (1u << k) : 0u;
-      a.chunk_cls[chunk] = m;
+    for (int i = 0; i < RG; i++) {
+      uint32_t c = 3;
+#pragma unroll
+      for (int k = 0; k < NC; k++) c = ((present[k] >> (r0 + i)) & 1) ? (uint32_t)k : c;
+      clsw |= c << (2 * i);
+    }
+    if (xi == 0) {  // every tile of chunk_or is stored (unmasked) here: all flags set
+      for (uint32_t i = lane; i < NC * a.nfw; i += 64) a.tflags[(size_t)chunk * NC * a.nfw + i] = ~0ull;
+      if (lane == 0) {
+        uint8_t m = 0;
+#pragma unroll
+        for (int k = 0; k < NC; k++) m |= present[k] ? (1u << k) : 0u;
+        a.chunk_cls[chunk] = m;
+      }
+      for (int i = lane; i < 3 * NC * (TW / 8); i += 64) (&orb[0][0][0])[i] = 0;
     }
     const uint32_t seg = chunk / a.seg_len;
-    const uint64_t ksimp = h32_mix(kSimpleZero);
-    uint64_t neq = 0;
+    const uint64_t *igp = IGN ? (const uint64_t *)a.ignore + w : nullptr;
+    uint64_t ig_next = IGN ? igp[0] : ~0ull;  // ignore word of the next tile (prefetched)
+    uint64_t nm = 0;                          // rows that differ from their predecessor
+    uint64_t ftw = 0, frel = ~0ull;           // first row's word / rel mask of the last tile
     auto transform_tile = [&](uint32_t t) {
       const int b = t % 3;
-      const uint64_t *ig = IGN ? (const uint64_t *)(a.ignore + (size_t)t * TW) : nullptr;
-      uint4 *row = &lds[b * TILE + lane * SLOTS];
-      uint64_t *krow = (uint64_t *)&kbuf[b * TILE];
-      const int sw = lane & 15;
-      uint64_t orw[NC];
+      const uint64_t igw = ig_next;
+      if (IGN) ig_next = igp[(size_t)min(t + 1, ntiles - 1) * (TW / 8)];
+      const uint64_t rel = IGN ? ~nonzero_bytes8(igw) : ~0ull;
+      uint64_t ow[NC];
 #pragma unroll
-      for (int k = 0; k < NC; k++) orw[k] = 0;
-      for (int q = xi; q < SLOTS; q += NX) {
-        uint4 *slot = &row[q ^ sw];
-        uint4 v = *slot;
-        bool dirty = false;
+      for (int k = 0; k < NC; k++) ow[k] = 0;
+      uint64_t prev = 0;
 #pragma unroll
-        for (int e = 0; e < 2; e++) {
-          const int wi = 2 * q + e;
-          const uint64_t x = ld_u64(v, e);
-          uint64_t kw;
-          if (__ballot(x != 0)) {
-            const uint64_t tw = xform8(x, xf);
-            if (e) { v.z = (uint32_t)tw; v.w = (uint32_t)(tw >> 32); }
-            else { v.x = (uint32_t)tw; v.y = (uint32_t)(tw >> 32); }
-            dirty = true;
-            kw = h32_mix(tw & (IGN ? ig[wi] : ~0ull));
+      for (int i = 0; i < RG; i++) {
+        const int r = r0 + i;
+        const int ad = r * SLOTS + ((w >> 1) ^ (r & 15));
+        uint64_t *p = (uint64_t *)&lds[b * TILE + ad] + (w & 1);
+        const uint64_t x = *p;
+        const uint32_t c = (clsw >> (2 * i)) & 3;
+        uint64_t tw;
+#ifdef KBZ_XP_NOCLS
+        if (MODE == KBZ_MODE_DYNAMORIO) tw = x;
+#else
+        if (MODE == KBZ_MODE_DYNAMORIO) tw = classify8(x);
+#endif
+        else if (c == 1 || c == 2) tw = simplify8(x);
+        else tw = (MODE == KBZ_MODE_AFL_CLASSIFY) ? classify8(x) : x;
+        if (X64) *p = tw;
+#ifdef KBZ_XP_NOMIX
+        ((uint64_t *)&kbuf[b * TILE + ad])[w & 1] = tw & igw;
+#else
+        ((uint64_t *)&kbuf[b * TILE + ad])[w & 1] = h32_mix(tw & igw);
+#endif
 #pragma unroll
-            for (int k = 0; k < NC; k++) {
-              if (present[k]) {
-                const uint64_t r = wave_or64((valid && cls == k) ? tw : 0);
-                orw[k] = (lane == wi) ? r : orw[k];
-              }
-            }
-            if (MODE == KBZ_MODE_DYNAMORIO) {
-              const uint64_t rel = IGN ? ~nonzero_bytes8(ig[wi]) : ~0ull;
-              neq |= (tw ^ from_prev_lane(tw)) & rel;
-            }
+        for (int k = 0; k < NC; k++) ow[k] |= (c == (uint32_t)k) ? tw : 0;
+        if (MODE == KBZ_MODE_DYNAMORIO) {
+          if (i == 0) {
+            ftw = tw;
           } else {
-            kw = simp ? ksimp : 0;
-            if (MODE != KBZ_MODE_DYNAMORIO) {
-#pragma unroll
-              for (int k = 1; k < NC; k++)  // simplified classes see 0x01 bytes everywhere
-                if (present[k]) orw[k] = (lane == wi) ? kSimpleZero : orw[k];
-            }
+            const uint64_t bal = __ballot(((tw ^ prev) & rel) != 0);
+            nm |= ((uint64_t)((uint32_t)bal != 0) << (r0a + i)) |
+                  ((uint64_t)((uint32_t)(bal >> 32) != 0) << (r0b + i));
           }
-          krow[(size_t)q * 2 * kChunk + 2 * lane + e] = kw;
+          prev = tw;
         }
-        if (X64 && dirty && (MODE != KBZ_MODE_AFL || simp)) *slot = v;
       }
-      // column ORs of this wave's words: lane wi holds word wi's OR
-      const bool mine = lane < TW / 8 && ((lane >> 1) % NX) == xi;
-      if (mine) {
+      if (MODE == KBZ_MODE_DYNAMORIO) {
+        bnd[t & 1][grp][w] = prev;
+        frel = rel;
+      }
 #pragma unroll
-        for (int k = 0; k < NC; k++)
-          if (present[k]) {
-            const size_t off = (size_t)k * a.map_size + (size_t)t * TW + (size_t)lane * 8;
-            *(uint64_t *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) = orw[k];
-            if (orw[k])
-              atomicOr((unsigned long long *)(a.segor + (size_t)seg * NC * a.map_size + off),
-                       (unsigned long long)orw[k]);
-          }
+      for (int k = 0; k < NC; k++)
+        if (present[k] && ow[k]) atomicOr((unsigned long long *)&orb[b][k][w], (unsigned long long)ow[k]);
+    };
+    // one step after tile t was transformed: group-boundary neighbour test, and X_0 stores
+    // the tile's column ORs
+    auto finish_tile = [&](uint32_t t) {
+      if (MODE == KBZ_MODE_DYNAMORIO) {
+        const uint64_t pl = grp > 0 ? bnd[t & 1][grp - 1][w] : 0;  // row 0: against 0
+        const uint64_t bal = __ballot(((ftw ^ pl) & frel) != 0);
+        nm |= ((uint64_t)((uint32_t)bal != 0) << r0a) |
+              ((uint64_t)((uint32_t)(bal >> 32) != 0) << r0b);
+      }
+      if (xi == 0 && lane < TW / 8) {
+        const int b = t % 3;
+#pragma unroll
+        for (int k = 0; k < NC; k++) {
+          if (!present[k]) continue;
+          const uint64_t o = orb[b][k][lane];
+          orb[b][k][lane] = 0;
+          const size_t off = (size_t)k * a.map_size + (size_t)t * TW + (size_t)lane * 8;
+          *(uint64_t *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) = o;
+          if (o)
+            atomicOr((unsigned long long *)(a.segor + (size_t)seg * NC * a.map_size + off),
+                     (unsigned long long)o);
+        }
       }
     };
     for (uint32_t g = 0; g < nsteps; g += D) {
       for (int u = 0; u < D; u++) {
         const uint32_t s = g + u;
+        if (s >= 2 && s - 2 < ntiles) finish_tile(s - 2);
         if (s >= 1 && s - 1 < ntiles) transform_tile(s - 1);
         lds_barrier();
       }
     }
-    neqs[xi][lane] = neq;
+    if (lane == 0) neqs[xi] = nm;
     lds_barrier();  // (Z)
   }
 }
@@ -1254,7 +1312,7 @@ void free_ctx(kbz_ctx *c) {
 }
 
 #ifndef KBZ_WIDE_NX
-#define KBZ_WIDE_NX 12
+#define KBZ_WIDE_NX 8
 #endif
 #ifndef KBZ_WIDE_NL
 #define KBZ_WIDE_NL 2
@@ -1262,6 +1320,10 @@ void free_ctx(kbz_ctx *c) {
 #ifndef KBZ_WIDE_D
 #define KBZ_WIDE_D 2
 #endif
+#ifndef KBZ_WIDE_ISO
+#define KBZ_WIDE_ISO 0
+#endif
+constexpr bool kWideISO = KBZ_WIDE_ISO;     // k_pass1w role layout (see there)
 constexpr int kWideNX = KBZ_WIDE_NX;        // transform waves of k_pass1w
 constexpr int kWideNL = KBZ_WIDE_NL;        // loader waves of k_pass1w
 constexpr int kWideD = KBZ_WIDE_D;          // their register ring depth
@@ -1299,8 +1361,8 @@ void launch_pass1(const Pass1Args &a, uint32_t chunks, hipStream_t s) {
   return launch_abl<MODE, IGN, X64, 0>(depth, a, chunks, s);
 #else
   if (pass1_is_wide(chunks))
-    hipLaunchKernelGGL((k_pass1w<MODE, IGN, X64, kWideNX, kWideNL, kWideD>), dim3(chunks),
-                       dim3(64 * (kWideNL + kWideNX)), 0, s, a);
+    hipLaunchKernelGGL((k_pass1w<MODE, IGN, X64, kWideNX, kWideNL, kWideD, kWideISO>),
+                       dim3(chunks), dim3(64 * (kWideNL + kWideNX + kWideISO)), 0, s, a);
   else
     hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, 0, KBZ_PASS1_DEPTH>), dim3(chunks), dim3(128), 0,
                        s, a);
@@ -1636,6 +1698,9 @@ int kbz_sync(kbz_ctx_t *c, void *stream) {
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   uint32_t cnt[4];
   HIP_TRY(hipMemcpy(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost));
+#if defined(KBZ_XP_NOMIX) || defined(KBZ_XP_NOCLS)
+  cnt[2] = 0;  // timing-only builds with inconsistent results
+#endif
   if (cnt[1] || cnt[2]) {  // sticky until reported here
     HIP_TRY(hipMemset(c->counters + 1, 0, 2 * sizeof(uint32_t)));
     return fail(cnt[1] ? "claim list overflow" : "inconsistent claim (internal error)");

@@ -26,7 +26,7 @@ for s in $STEPS; do
     prof)
       echo "== rocprofv3 $(date +%T)"
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run \
-        -- python3 bench.py --steps 10 --warmup 2 --no-cpu ${BENCH_ARGS:-} > $OUT/prof.log 2>&1
+        -- python3 bench.py --steps 40 --warmup 2 --no-cpu ${BENCH_ARGS:-} > $OUT/prof.log 2>&1
       rc=$?; tail -3 $OUT/prof.log; [ $rc -eq 0 ] || exit $rc
       find $OUT/prof -name "*stats*.csv" | head -5 ;;
     pmc)
