@@ -108,6 +108,23 @@ int kbz_triage_batch_host(kbz_ctx_t *ctx, const uint8_t *traces, size_t n, size_
                           const int8_t *outcome, uint8_t *hnb_out, uint32_t *h32_out,
                           uint64_t *x64_out, int want);
 
+/* Pinned ingest ring (zero-copy producer path; SURVEY.md §8(b) kbz_ring_acquire/submit).  The
+ * producer -- e.g. the fuzz loop copying each exec's trace_bits (fuzzer/main.c:370-418,
+ * afl_instrumentation.c:153-180) -- writes rows straight into a pinned slot, so no staging copy
+ * precedes the H2D transfer; two slots alternate, so filling one overlaps the GPU's work on the
+ * other.  Batches are triaged in submission order against the carried virgin state.
+ *   kbz_ring_acquire: waits until the next slot's previous batch is done (delivering its
+ *     results), returns its rows (cap rows of map_size bytes, stride map_size) and outcome array.
+ *   kbz_ring_submit: triages the slot's first n rows (outcome array used if have_outcome);
+ *     returns at once.  hnb_out/h32_out/x64_out are host buffers (NULL = not wanted), filled
+ *     when the slot is acquired again or at kbz_ring_flush.
+ *   kbz_ring_flush: waits for every submitted batch, delivers results, reports device errors.
+ * Do not interleave with kbz_triage_batch_host on the same context (they share the slots). */
+int kbz_ring_acquire(kbz_ctx_t *ctx, uint8_t **rows, int8_t **outcome, size_t *cap);
+int kbz_ring_submit(kbz_ctx_t *ctx, size_t n, int have_outcome, uint8_t *hnb_out,
+                    uint32_t *h32_out, uint64_t *x64_out, int want);
+int kbz_ring_flush(kbz_ctx_t *ctx);
+
 /* ---- sharded (multi-GPU) triage ------------------------------------------------------------ */
 /* A batch split into contiguous shards, one per GPU (rank g holds traces [lo_g, hi_g)), gives
  * the same results as one kbz_triage_batch over the whole batch when each rank runs:

@@ -29,6 +29,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kbz_device.h"
@@ -1253,6 +1254,20 @@ struct kbz_ctx {
   uint64_t *dres_x64 = nullptr;
   size_t slot_rows = 0;
   hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_used[2] = {nullptr, nullptr};
+  // pinned ingest ring (kbz_ring_*): per slot, device + pinned results and the pending
+  // delivery of the batch last submitted from it
+  struct RingSlot {
+    uint8_t *d_hnb = nullptr, *h_hnb = nullptr;
+    uint32_t *d_h32 = nullptr, *h_h32 = nullptr;
+    uint64_t *d_x64 = nullptr, *h_x64 = nullptr;
+    size_t n = 0;
+    bool pending = false;
+    uint8_t *hnb_out = nullptr;
+    uint32_t *h32_out = nullptr;
+    uint64_t *x64_out = nullptr;
+  } ring[2];
+  int ring_next = 0;        // slot the next kbz_ring_acquire returns
+  int ring_acquired = -1;   // slot handed out and not yet submitted
 };
 
 namespace {
@@ -1301,6 +1316,11 @@ void free_ctx(kbz_ctx *c) {
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (int i = 0; i < 2; i++) {
+    auto &r = c->ring[i];
+    for (void *p : {(void *)r.d_hnb, (void *)r.d_h32, (void *)r.d_x64})
+      if (p) (void)hipFree(p);
+    for (void *p : {(void *)r.h_hnb, (void *)r.h_h32, (void *)r.h_x64})
+      if (p) (void)hipHostFree(p);
     if (c->pin[i]) (void)hipHostFree(c->pin[i]);
     if (c->pin_oc[i]) (void)hipHostFree(c->pin_oc[i]);
     if (c->ev_copied[i]) (void)hipEventDestroy(c->ev_copied[i]);
@@ -1731,6 +1751,25 @@ int ensure_streaming(kbz_ctx *c) {
   HIP_TRY(hipMalloc((void **)&c->dres_x64, c->max_batch * 8));
   return 0;
 }
+
+// Rows [0, cnt) of a host batch into a pinned slot, split over several host threads: one
+// thread's memcpy from pageable memory runs well below PCIe Gen5 rate, so a single copier would
+// bound the streaming path (KBZ_FILL_THREADS, default 8).
+void fill_slot(uint8_t *dst, const uint8_t *src, size_t cnt, size_t stride, size_t M) {
+  static const int nt = std::max(1, std::min(64, getenv("KBZ_FILL_THREADS")
+                                                     ? atoi(getenv("KBZ_FILL_THREADS")) : 8));
+  auto part = [=](size_t r0, size_t r1) {
+    if (stride == M) memcpy(dst + r0 * M, src + r0 * M, (r1 - r0) * M);
+    else
+      for (size_t r = r0; r < r1; r++) memcpy(dst + r * M, src + r * stride, M);
+  };
+  const size_t T = std::min<size_t>(nt, std::max<size_t>(1, cnt * M >> 22));  // >= 4 MiB each
+  if (T <= 1) return part(0, cnt);
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < T; i++) th.emplace_back(part, cnt * i / T, cnt * (i + 1) / T);
+  part(0, cnt / T);
+  for (auto &t : th) t.join();
+}
 }  // namespace
 
 int kbz_triage_batch_host(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride,
@@ -1749,11 +1788,7 @@ int kbz_triage_batch_host(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t 
     const int sl = (int)(b & 1);
     const size_t lo = b * R, cnt = std::min(R, n - lo);
     HIP_TRY(hipEventSynchronize(c->ev_used[sl]));  // slot free (no-op the first time)
-    if (stride == M) {
-      memcpy(c->pin[sl], traces + lo * M, cnt * M);
-    } else {
-      for (size_t r = 0; r < cnt; r++) memcpy(c->pin[sl] + r * M, traces + (lo + r) * stride, M);
-    }
+    fill_slot(c->pin[sl], traces + lo * stride, cnt, stride, M);
     if (outcome) memcpy(c->pin_oc[sl], outcome + lo, cnt);
     HIP_TRY(hipMemcpyAsync(c->dslot[sl], c->pin[sl], cnt * M, hipMemcpyHostToDevice,
                            c->copy_stream));
@@ -1775,6 +1810,99 @@ int kbz_triage_batch_host(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t 
     if (x64_out && (want & KBZ_WANT_X64))
       HIP_TRY(hipMemcpy(x64_out, c->dres_x64, n * 8, hipMemcpyDeviceToHost));
   }
+  return kbz_sync(c, c->work_stream);
+}
+
+// ---- pinned ingest ring ------------------------------------------------------------------------
+// The producer (the fuzz loop copying each exec's trace_bits, fuzzer/main.c:370-418 in batched
+// form) writes straight into one of two pinned slots; submit queues the slot's H2D copy, the
+// triage and the D2H copy of its results, and returns.  While the GPU works on one slot the
+// producer fills the other.  Results reach the caller's buffers when that slot is acquired again
+// (its previous batch is then complete) or at kbz_ring_flush.
+namespace {
+int ensure_ring(kbz_ctx *c) {
+  if (ensure_streaming(c)) return -1;
+  const size_t R = c->slot_rows;
+  for (auto &r : c->ring) {
+    if (r.d_hnb) continue;
+    HIP_TRY(hipMalloc((void **)&r.d_hnb, R));
+    HIP_TRY(hipMalloc((void **)&r.d_h32, R * 4));
+    HIP_TRY(hipMalloc((void **)&r.d_x64, R * 8));
+    HIP_TRY(hipHostMalloc((void **)&r.h_hnb, R, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void **)&r.h_h32, R * 4, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void **)&r.h_x64, R * 8, hipHostMallocDefault));
+  }
+  return 0;
+}
+// the slot's batch is complete (its ev_used has been waited for): hand its results over
+void ring_deliver(kbz_ctx::RingSlot &r) {
+  if (!r.pending) return;
+  if (r.hnb_out) memcpy(r.hnb_out, r.h_hnb, r.n);
+  if (r.h32_out) memcpy(r.h32_out, r.h_h32, r.n * 4);
+  if (r.x64_out) memcpy(r.x64_out, r.h_x64, r.n * 8);
+  r.pending = false;
+}
+}  // namespace
+
+int kbz_ring_acquire(kbz_ctx_t *c, uint8_t **rows, int8_t **outcome, size_t *cap) {
+  if (!c || !rows) return fail("null argument");
+  if (c->ring_acquired >= 0) return fail("kbz_ring_acquire: previous slot not submitted");
+  DevGuard g(c->device);
+  if (ensure_ring(c)) return -1;
+  const int sl = c->ring_next;
+  HIP_TRY(hipEventSynchronize(c->ev_used[sl]));  // its previous batch is done
+  ring_deliver(c->ring[sl]);
+  c->ring_acquired = sl;
+  *rows = c->pin[sl];
+  if (outcome) *outcome = c->pin_oc[sl];
+  if (cap) *cap = c->slot_rows;
+  return 0;
+}
+
+int kbz_ring_submit(kbz_ctx_t *c, size_t n, int have_outcome, uint8_t *hnb_out,
+                    uint32_t *h32_out, uint64_t *x64_out, int want) {
+  if (!c) return fail("null ctx");
+  const int sl = c->ring_acquired;
+  if (sl < 0) return fail("kbz_ring_submit: no slot acquired");
+  if (n > c->slot_rows) return fail("kbz_ring_submit: n exceeds the slot capacity");
+  DevGuard g(c->device);
+  auto &r = c->ring[sl];
+  const size_t M = c->M;
+  HIP_TRY(hipMemcpyAsync(c->dslot[sl], c->pin[sl], n * M, hipMemcpyHostToDevice, c->copy_stream));
+  if (have_outcome)
+    HIP_TRY(hipMemcpyAsync(c->dslot_oc[sl], c->pin_oc[sl], n, hipMemcpyHostToDevice,
+                           c->copy_stream));
+  HIP_TRY(hipEventRecord(c->ev_copied[sl], c->copy_stream));
+  HIP_TRY(hipStreamWaitEvent(c->work_stream, c->ev_copied[sl], 0));
+  const bool x64 = (want & KBZ_WANT_X64) && x64_out;
+  if (kbz_triage_batch_device(c, c->dslot[sl], n, M, have_outcome ? c->dslot_oc[sl] : nullptr,
+                              r.d_hnb, h32_out ? r.d_h32 : nullptr, x64 ? r.d_x64 : nullptr,
+                              want, c->work_stream))
+    return -1;
+  if (n) {
+    HIP_TRY(hipMemcpyAsync(r.h_hnb, r.d_hnb, n, hipMemcpyDeviceToHost, c->work_stream));
+    if (h32_out)
+      HIP_TRY(hipMemcpyAsync(r.h_h32, r.d_h32, n * 4, hipMemcpyDeviceToHost, c->work_stream));
+    if (x64)
+      HIP_TRY(hipMemcpyAsync(r.h_x64, r.d_x64, n * 8, hipMemcpyDeviceToHost, c->work_stream));
+  }
+  HIP_TRY(hipEventRecord(c->ev_used[sl], c->work_stream));
+  r.n = n;
+  r.hnb_out = hnb_out;
+  r.h32_out = h32_out;
+  r.x64_out = x64 ? x64_out : nullptr;
+  r.pending = true;
+  c->ring_acquired = -1;
+  c->ring_next = sl ^ 1;
+  return 0;
+}
+
+int kbz_ring_flush(kbz_ctx_t *c) {
+  if (!c) return fail("null ctx");
+  if (!c->work_stream) return 0;  // nothing was ever submitted
+  DevGuard g(c->device);
+  HIP_TRY(hipStreamSynchronize(c->work_stream));
+  for (auto &r : c->ring) ring_deliver(r);
   return kbz_sync(c, c->work_stream);
 }
 

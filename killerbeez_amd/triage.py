@@ -155,6 +155,28 @@ class TriageContext:
             res["x64"] = x64
         return res
 
+    # -- pinned ingest ring (zero-copy producer path; include/kbz_triage.h kbz_ring_*) ------
+    def ring_acquire(self):
+        """-> (rows, outcome): numpy views of the next pinned slot, uint8 [cap, map_size] and
+        int8 [cap].  Blocks until that slot's previous batch is done."""
+        rows, oc, cap = C.c_void_p(), C.c_void_p(), C.c_size_t()
+        check(lib().kbz_ring_acquire(self._h, C.byref(rows), C.byref(oc), C.byref(cap)),
+              "kbz_ring_acquire")
+        n = cap.value
+        r = np.ctypeslib.as_array(C.cast(rows, C.POINTER(C.c_uint8)), shape=(n, self.map_size))
+        o = np.ctypeslib.as_array(C.cast(oc, C.POINTER(C.c_int8)), shape=(n,))
+        return r, o
+
+    def ring_submit(self, n, have_outcome=True, hnb_out=None, h32_out=None, x64_out=None,
+                    want: int = WANT_H32):
+        """Queue the slot's first n rows; the numpy result buffers are filled when the slot is
+        acquired again or at ring_flush (keep them alive until then)."""
+        check(lib().kbz_ring_submit(self._h, n, int(bool(have_outcome)), _np_ptr(hnb_out),
+                                    _np_ptr(h32_out), _np_ptr(x64_out), want), "kbz_ring_submit")
+
+    def ring_flush(self):
+        check(lib().kbz_ring_flush(self._h), "kbz_ring_flush")
+
     # -- sharded triage (one rank's part; see killerbeez_amd.dist) --------------------------
     def shard_begin(self, traces, outcome=None, want=WANT_H32, out=None, stream=None):
         import torch

@@ -323,3 +323,39 @@ def test_sharded_protocol_on_gpu(gpu, mode, counts):
                 assert c.last_hash == exp["last_hash"]
         v, last = exp["virgin"], exp.get("last_hash", 0)
         assert batch == 0 or 0 < (hnb > 0).sum() < n  # later batches still find something
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_ingest_ring(gpu, mode):
+    """kbz_ring_*: the producer writes rows into pinned slots, batches are queued back to back
+    (results delivered on re-acquire / flush) and equal one sequential pass over all traces."""
+    m, sizes = 4096, [300, 17, 0, 256, 1, 300]
+    ctx = TriageContext(m, mode, 300)
+    t, oc = synth.sparse_np(sum(sizes), m, seed=77, hot_frac=0.05)
+    t[301] = t[300]  # DynamoRIO skip across a batch boundary
+    oc[300:317] = oracle.FUZZ_NONE  # batch 1 is submitted without an outcome array
+    exp = oracle.triage_batch(mode, t, oc, virgin=ctx.get_virgin(), last_hash=ctx.last_hash,
+                              want=oracle.WANT_H32 | oracle.WANT_X64)
+    outs, lo = [], 0
+    for i, n in enumerate(sizes):
+        rows, ocs = ctx.ring_acquire()
+        assert rows.shape[0] >= n and rows.shape[1] == m
+        rows[:n] = t[lo:lo + n]
+        ocs[:n] = oc[lo:lo + n]
+        hnb = np.full(n, 0xEE, np.uint8)
+        h32 = np.zeros(n, np.uint32)
+        x64 = np.zeros(n, np.uint64)
+        if i == 1:
+            ocs[:n] = -7  # stale slot contents must not be read without have_outcome
+        ctx.ring_submit(n, i != 1, hnb, h32, x64, WANT_H32 | WANT_X64)
+        outs.append((lo, n, hnb, h32, x64))
+        lo += n
+    ctx.ring_flush()
+    for lo, n, hnb, h32, x64 in outs:
+        np.testing.assert_array_equal(hnb, exp["hnb"][lo:lo + n])
+        np.testing.assert_array_equal(h32, exp["h32"][lo:lo + n])
+        np.testing.assert_array_equal(x64, exp["x64"][lo:lo + n])
+    np.testing.assert_array_equal(ctx.get_virgin(), exp["virgin"])
+    if mode == MODE_DYNAMORIO:
+        assert ctx.last_hash == exp["last_hash"]
+    ctx.close()
