@@ -20,6 +20,10 @@
  *   kbz_merge_and_device / kbz_merge_and_host
  *       the merger fold merger/merger.c:79-99 -> afl_merge afl_instrumentation.c:123-140
  *       (merge_bitmaps :116-121 == dynamorio_instrumentation.c:334-339)
+ *   kbz_triage_modules_device
+ *       has_new_coverage_per_module (dynamorio_instrumentation.c:1477-1493): per-module maps
+ *   kbz_picker_ignore_device
+ *       the picker CLI's ignore-bytes diff across repeated runs (picker/main.c:240-262)
  *   kbz_hash32_device / kbz_xxh64_device
  *       afl_progs/hash.h:36-65 (hash32) and instrumentation/xxhash.c:855 (XXH64, v0.6.5)
  *       over every trace of a batch (crash/hang dedup keys).
@@ -170,6 +174,31 @@ int kbz_merge_and_device(uint8_t *out, const uint8_t *states, size_t n, size_t s
                          void *stream);
 /* Host variant: streams host states (pageable or pinned) through the device. Synchronous. */
 int kbz_merge_and_host(uint8_t *out, const uint8_t *states, size_t n, size_t state_bytes);
+
+/* ---- DynamoRIO per-module coverage ----------------------------------------------------------- */
+/* has_new_coverage_per_module (dynamorio_instrumentation.c:1477-1493) over an ordered batch: each
+ * traced module m has its own context ctxs[m] (its virgin map, ignore bytes and last hash, as
+ * target_module_t holds them, dynamorio_instrumentation.h:26-83) and its own map inside every
+ * trace row, at traces + j*stride + module_offsets[m] (host size_t[k], 16-byte aligned).
+ * hnb_out: device uint8[k*n], hnb_out[m*n + j] = module m's has_new_coverage result for exec j
+ * (0/1/2; nonzero = last_path_was_new); any_out: device uint8[n] or NULL, the OR over modules
+ * (the per-exec return value).  Stream-ordered. */
+int kbz_triage_modules_device(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *traces, size_t n,
+                              size_t stride, const size_t *module_offsets, const int8_t *outcome,
+                              uint8_t *hnb_out, uint8_t *any_out, void *stream);
+
+/* ---- picker: ignore bytes from repeated runs ------------------------------------------------ */
+/* The picker's diff loop (picker/main.c:240-262) for one module: runs = device
+ * [files][iters][size] bytes, the instrumentation data of iteration `it` of input file `f`
+ * (picker/main.c:209 layout).  ignore_out (device, size bytes) = 0x00 where two consecutive
+ * iterations of one file differ (a noisy byte), 0xff elsewhere -- the ignore_bytes file the
+ * DynamoRIO plugin loads (kbz_set_ignore).  pair_counts_out (device uint32[files*(iters-1)] or
+ * NULL): differing bytes of each (it-1, it) pair (the reference's ignore_count); total_out
+ * (device uint64 or NULL): noisy bytes (total_ignore_count).  size and both pointers must be
+ * multiples of 16 / 16-byte aligned.  Stream-ordered. */
+int kbz_picker_ignore_device(const uint8_t *runs, size_t files, size_t iters, size_t size,
+                             uint8_t *ignore_out, uint32_t *pair_counts_out, uint64_t *total_out,
+                             void *stream);
 
 /* ---- standalone hashes over a batch --------------------------------------------------------- */
 /* h32_out[j] = hash32(row j, len, seed); x64_out[j] = XXH64(row j, len, seed).  len % 8 == 0

@@ -41,6 +41,8 @@ SIGNATURES = [
     ("kbz_or_reduce", _i, [_vp, _vp, _sz, _sz, _sz, _vp]),
     ("kbz_merge_and_device", _i, [_vp, _vp, _sz, _sz, _vp]),
     ("kbz_merge_and_host", _i, [_vp, _vp, _sz, _sz]),
+    ("kbz_triage_modules_device", _i, [_vp, _sz, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp]),
+    ("kbz_picker_ignore_device", _i, [_vp, _sz, _sz, _sz, _vp, _vp, _vp, _vp]),
     ("kbz_hash32_device", _i, [_vp, _sz, _sz, _sz, _u32, _vp, _vp]),
     ("kbz_xxh64_device", _i, [_vp, _sz, _sz, _sz, _u64, _vp, _vp]),
     ("kbz_sync", _i, [_vp, _vp]),

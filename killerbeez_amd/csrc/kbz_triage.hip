@@ -1138,6 +1138,72 @@ __global__ void k_and_bytes(const uint8_t *states, size_t n, size_t state_bytes,
   out[b] = acc;
 }
 
+// per-module combine (dynamorio_instrumentation.c:1477-1493): any[j] = OR over modules of hnb != 0
+__global__ __launch_bounds__(256) void k_modules_any(const uint8_t *hnb, size_t k, size_t n,
+                                                     uint8_t *any) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  uint8_t r = 0;
+  for (size_t m = 0; m < k; m++) r |= hnb[m * n + j] != 0;
+  any[j] = r;
+}
+
+// ---- picker: ignore-bytes diff across repeated runs (picker/main.c:240-262) --------------------
+// 0x80 in every nonzero byte of x
+__device__ __forceinline__ uint32_t nz_bytes32(uint32_t x) {
+  return (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+// grid (columns of 16 B / 256, files): per 16-B column, XOR of consecutive iterations of one
+// file (each row read once, the previous one kept in registers); the OR of the differences goes
+// to diff (zeroed, u32 atomics, nonzero words only); pair_counts[f*(iters-1) + it-1] += differing
+// bytes of this wave's 1 KiB (one atomic per wave per pair).
+__global__ __launch_bounds__(256) void k_picker_diff(const uint8_t *runs, size_t files, size_t iters,
+                                                     size_t size, uint32_t *diff,
+                                                     uint32_t *pair_counts) {
+  const size_t col = (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  const bool in = col < size;
+  for (size_t f = blockIdx.y; f < files; f += gridDim.y) {
+    const uint8_t *base = runs + f * iters * size + (in ? col : 0);
+    uint4 prev = in ? ld_stream16(base) : make_uint4(0, 0, 0, 0);
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (size_t it = 1; it < iters; it++) {
+      const uint4 cur = in ? ld_stream16(base + it * size) : make_uint4(0, 0, 0, 0);
+      const uint4 d = make_uint4(prev.x ^ cur.x, prev.y ^ cur.y, prev.z ^ cur.z, prev.w ^ cur.w);
+      acc = or4(acc, d);
+      const uint32_t c = __popc(nz_bytes32(d.x)) + __popc(nz_bytes32(d.y)) +
+                         __popc(nz_bytes32(d.z)) + __popc(nz_bytes32(d.w));
+      const uint32_t tot = wave_sum32(c);
+      if (pair_counts && (threadIdx.x & 63) == 0 && tot)
+        atomicAdd(pair_counts + f * (iters - 1) + it - 1, tot);
+      prev = cur;
+    }
+    if (in) {
+      uint32_t *dw = diff + col / 4;
+      if (acc.x) atomicOr(dw + 0, acc.x);
+      if (acc.y) atomicOr(dw + 1, acc.y);
+      if (acc.z) atomicOr(dw + 2, acc.z);
+      if (acc.w) atomicOr(dw + 3, acc.w);
+    }
+  }
+}
+// in place: a byte that differed anywhere -> 0x00 (ignore), else 0xff; counts the noisy bytes
+__global__ __launch_bounds__(256) void k_picker_final(uint32_t *words, size_t nwords,
+                                                      unsigned long long *total) {
+  const size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t nz = 0;
+  if (w < nwords) {
+    nz = nz_bytes32(words[w]);
+    words[w] = ~((nz >> 7) * 0xffu);
+  }
+  const uint32_t c = wave_sum32(__popc(nz));
+  if (total && (threadIdx.x & 63) == 0 && c) atomicAdd(total, (unsigned long long)c);
+}
+
 // ---- standalone row hashes (utility path: one lane per row, direct loads) ---------------------
 __global__ void k_rowhash32(const uint8_t *rows, size_t n, size_t stride, size_t len, uint32_t seed,
                             uint32_t *out) {
@@ -2005,6 +2071,58 @@ int kbz_merge_and_host(uint8_t *out, const uint8_t *states, size_t n, size_t sta
 }
 
 // ---- standalone hashes ---------------------------------------------------------------------------
+// ---- DynamoRIO per-module coverage ------------------------------------------------------------
+int kbz_triage_modules_device(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *traces, size_t n,
+                              size_t stride, const size_t *module_offsets, const int8_t *outcome,
+                              uint8_t *hnb_out, uint8_t *any_out, void *stream) {
+  if (!ctxs || (k && !module_offsets) || (n && !hnb_out)) return fail("null argument");
+  for (size_t m = 0; m < k; m++) {
+    if (!ctxs[m]) return fail("kbz_triage_modules_device: null context");
+    if (module_offsets[m] + ctxs[m]->M > stride)
+      return fail("kbz_triage_modules_device: module map exceeds the row stride");
+    if (module_offsets[m] & 15) return fail("kbz_triage_modules_device: offset not 16-byte aligned");
+  }
+  for (size_t m = 0; m < k; m++)
+    if (kbz_triage_batch_device(ctxs[m], traces + module_offsets[m], n, stride, outcome,
+                                hnb_out + m * n, nullptr, nullptr, KBZ_WANT_H32, stream))
+      return -1;
+  if (any_out && n) {
+    hipStream_t s = (hipStream_t)stream;
+    if (k == 0) {
+      HIP_TRY(hipMemsetAsync(any_out, 0, n, s));
+      return 0;
+    }
+    hipLaunchKernelGGL(k_modules_any, dim3(cdiv(n, 256)), dim3(256), 0, s, hnb_out, k, n, any_out);
+    HIP_TRY(hipGetLastError());
+  }
+  return 0;
+}
+
+// ---- picker -----------------------------------------------------------------------------------
+int kbz_picker_ignore_device(const uint8_t *runs, size_t files, size_t iters, size_t size,
+                             uint8_t *ignore_out, uint32_t *pair_counts_out, uint64_t *total_out,
+                             void *stream) {
+  if (!ignore_out || (!runs && files && iters)) return fail("null argument");
+  if ((size & 15) || ((uintptr_t)runs & 15) || ((uintptr_t)ignore_out & 15))
+    return fail("kbz_picker_ignore_device: size and pointers must be 16-byte multiples/aligned");
+  if (size == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemsetAsync(ignore_out, 0, size, s));
+  if (total_out) HIP_TRY(hipMemsetAsync(total_out, 0, sizeof(uint64_t), s));
+  if (files && iters >= 2) {
+    if (pair_counts_out)
+      HIP_TRY(hipMemsetAsync(pair_counts_out, 0, files * (iters - 1) * sizeof(uint32_t), s));
+    hipLaunchKernelGGL(k_picker_diff, dim3(cdiv(size / 16, 256), (unsigned)std::min<size_t>(files, 65535)),
+                       dim3(256), 0, s, runs, files, iters, size, (uint32_t *)ignore_out,
+                       pair_counts_out);
+    HIP_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_picker_final, dim3(cdiv(size / 4, 256)), dim3(256), 0, s,
+                     (uint32_t *)ignore_out, size / 4, (unsigned long long *)total_out);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 int kbz_hash32_device(const uint8_t *rows, size_t n, size_t stride, size_t len, uint32_t seed,
                       uint32_t *h32_out, void *stream) {
   if (len % 8) return fail("hash32 needs len % 8 == 0 (afl_progs/hash.h:38)");

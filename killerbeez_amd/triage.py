@@ -262,6 +262,47 @@ def merge_and_host(states: np.ndarray) -> np.ndarray:
     return out
 
 
+def triage_modules(ctxs, traces, offsets, outcome=None, stream=None):
+    """DynamoRIO per-module coverage (has_new_coverage_per_module,
+    dynamorio_instrumentation.c:1477-1493) over an ordered batch.  ctxs: one TriageContext per
+    module; traces: CUDA uint8 [n, row_bytes] holding every module's map at offsets[m].
+    Returns (hnb [k, n] uint8 per module, any [n] uint8: OR over modules)."""
+    import torch
+
+    n, k = traces.shape[0], len(ctxs)
+    hs = (C.c_void_p * max(k, 1))(*[c.handle for c in ctxs])
+    offs = (C.c_size_t * max(k, 1))(*offsets)
+    hnb = torch.empty((k, n), dtype=torch.uint8, device=traces.device)
+    anyv = torch.empty(n, dtype=torch.uint8, device=traces.device)
+    oc = None if outcome is None else C.c_void_p(outcome.data_ptr())
+    check(lib().kbz_triage_modules_device(hs, k, C.c_void_p(traces.data_ptr()) if n else None,
+                                          n, traces.stride(0), offs, oc,
+                                          C.c_void_p(hnb.data_ptr()) if n else None,
+                                          C.c_void_p(anyv.data_ptr()) if n else None,
+                                          _stream_handle(stream)), "kbz_triage_modules_device")
+    return hnb, anyv
+
+
+def picker_ignore(runs, stream=None):
+    """The picker's ignore-bytes diff (picker/main.c:240-262) for one module.  runs: CUDA uint8
+    [files, iters, size] (size % 16 == 0).  Returns (ignore [size] uint8: 0x00 = noisy byte,
+    0xff = keep; pair_counts [files, iters-1] int32: differing bytes per consecutive pair;
+    total: 0-d int64 tensor, the number of noisy bytes), all on the device."""
+    import torch
+
+    files, iters, size = runs.shape
+    runs = runs.contiguous()
+    ign = torch.empty(size, dtype=torch.uint8, device=runs.device)
+    pc = torch.empty((files, max(iters - 1, 0)), dtype=torch.int32, device=runs.device)
+    tot = torch.empty((), dtype=torch.int64, device=runs.device)
+    check(lib().kbz_picker_ignore_device(C.c_void_p(runs.data_ptr()) if runs.numel() else None,
+                                         files, iters, size, C.c_void_p(ign.data_ptr()),
+                                         C.c_void_p(pc.data_ptr()) if pc.numel() else None,
+                                         C.c_void_p(tot.data_ptr()), _stream_handle(stream)),
+          "kbz_picker_ignore_device")
+    return ign, pc, tot
+
+
 def or_reduce(out, stacked, r_lo, r_hi, nbytes, stream=None):
     check(lib().kbz_or_reduce(C.c_void_p(out.data_ptr()), C.c_void_p(stacked.data_ptr()), r_lo,
                               r_hi, nbytes, _stream_handle(stream)), "kbz_or_reduce")

@@ -67,6 +67,9 @@ def lib():
         L.kbzo_xxh64.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
         L.kbzo_merge_and.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.kbzo_merge_many.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t]
+        L.kbzo_picker_ignore.restype = C.c_size_t
+        L.kbzo_picker_ignore.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t,
+                                         C.c_void_p, C.c_void_p]
         args = [C.c_int, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_void_p,
                 C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                 C.c_void_p]
@@ -111,6 +114,9 @@ def ref():
         R.ref_xxh64_ref.restype = C.c_uint64
         R.ref_xxh64_ref.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
         R.ref_xxh_version_ref.restype = C.c_uint
+        R.ref_picker_ignore_ref.restype = C.c_int
+        R.ref_picker_ignore_ref.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                            C.c_void_p]
         _ref = R
     return _ref
 
@@ -162,3 +168,14 @@ def merge_many(states: np.ndarray) -> np.ndarray:
     out = np.empty(per, np.uint8)
     lib().kbzo_merge_many(_p(out), _p(s), n, per)
     return out.reshape(s.shape[1:])
+
+
+def picker_ignore(runs: np.ndarray):
+    """Restated picker diff (picker/main.c:240-262) over runs [files, iters, size]:
+    (ignore [size], pair_counts [files, iters-1] uint32, total)."""
+    r = np.ascontiguousarray(runs, dtype=np.uint8)
+    files, iters, size = r.shape
+    ign = np.empty(size, np.uint8)
+    pc = np.zeros((files, max(iters - 1, 0)), np.uint32)
+    tot = lib().kbzo_picker_ignore(_p(r), files, iters, size, _p(ign), _p(pc) if pc.size else None)
+    return ign, pc, int(tot)

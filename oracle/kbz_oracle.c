@@ -364,3 +364,29 @@ void kbzo_merge_many(uint8_t *dest, const uint8_t *states, size_t n, size_t stat
   memset(dest, 0xff, state_bytes);
   for (size_t s = 0; s < n; s++) kbzo_merge_and(dest, states + s * state_bytes, state_bytes);
 }
+
+/* Picker ignore-bytes diff (picker/main.c:240-262): for one module, runs[f][it][size] holds
+ * the instrumentation data of iteration `it` of file `f`.  A byte is noisy (ignore 0x00) if
+ * any two consecutive iterations of the same file differ there; every other byte stays 0xff.
+ * pair_counts[f*(iters-1) + it-1] = bytes differing between iterations it-1 and it (the
+ * reference's per-pair ignore_count, :246-258); returns the number of noisy bytes (its
+ * total_ignore_count, :254-255). */
+size_t kbzo_picker_ignore(const uint8_t *runs, size_t files, size_t iters, size_t size,
+                          uint8_t *ignore, uint32_t *pair_counts) {
+  size_t total = 0;
+  memset(ignore, 0xff, size);
+  for (size_t f = 0; f < files; f++) {
+    for (size_t it = 1; it < iters; it++) {
+      const uint8_t *prev = runs + (f * iters + it - 1) * size, *cur = prev + size;
+      uint32_t cnt = 0;
+      for (size_t i = 0; i < size; i++) {
+        if (prev[i] == cur[i]) continue;
+        total += ignore[i] != 0;
+        ignore[i] = 0;
+        cnt++;
+      }
+      if (pair_counts) pair_counts[f * (iters - 1) + it - 1] = cnt;
+    }
+  }
+  return total;
+}

@@ -53,6 +53,12 @@ int kbzo_triage_batch_mt(int mode, const uint8_t *traces, size_t n, size_t strid
 /* Merger fold (merger/merger.c:79-99): dest = AND of n states, each `state_bytes` long. */
 void kbzo_merge_many(uint8_t *dest, const uint8_t *states, size_t n, size_t state_bytes);
 
+/* Picker ignore-bytes diff (picker/main.c:240-262) over runs[files][iters][size]: ignore = 0x00
+ * where consecutive iterations of a file differ, else 0xff; per-pair differing-byte counts;
+ * returns the number of noisy bytes. */
+size_t kbzo_picker_ignore(const uint8_t *runs, size_t files, size_t iters, size_t size,
+                          uint8_t *ignore, uint32_t *pair_counts);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,6 +13,9 @@
  *             :600-707 (has_new_bits, simplify_lookup, simplify_trace)   [x86_64 variants]
  *   REF_DR    instrumentation/dynamorio_instrumentation.c:79-339 (has_new_bits,
  *             has_new_bits_with_ignore, count_class_lookup, classify_counts, merge_bitmaps)
+ *   REF_PICKER picker/main.c:240-262 (the ignore-bytes diff loop of the picker CLI, Win32 main()
+ *             otherwise); its per-pair DEBUG_MSG (:260) is defined here to record the
+ *             reference's own ignore_count / total_ignore_count instead of logging
  *   REF_HASH  afl_progs/hash.h:36-65 (hash32) and instrumentation/winafl_hash.h:80-112
  *             (hash32_with_ignore), instrumentation/xxhash.h + xxhash.c:855 (XXH64, v0.6.5)
  * MAP_SIZE is a compile-time constant in the reference (afl_progs/config.h:314-315); the
@@ -77,6 +80,21 @@ void REF_NAME(ref_dr_triage_loop)(const uint8_t *traces, size_t n, size_t stride
   *last_hash = last;
 }
 
+#elif defined(REF_PICKER)
+/* One module's runs: module_infos[(file*num_iterations + iteration)*module_info_size], the
+ * layout of picker/main.c:209.  pair_counts[file*(num_iterations-1) + iteration-1] receives the
+ * reference's ignore_count of that pair; returns its final total_ignore_count. */
+static unsigned *ref_pair_counts;
+#define DEBUG_MSG(fmt, mod, file, prev_it, cur_it, ic, tic) \
+  (ref_pair_counts ? (void)(ref_pair_counts[file_count * (num_iterations - 1) + iteration - 1] = (ic)) : (void)0)
+int REF_NAME(ref_picker_ignore)(char *module_infos, int num_files, int num_iterations,
+                               int module_info_size, char *ignore_bytes, unsigned *pair_counts) {
+  int index = 0, file_count, iteration, i;
+  ref_pair_counts = pair_counts;
+#include "picker_diff.inc"
+  ref_pair_counts = 0;
+  return total_ignore_count;
+}
 #elif defined(REF_HASH)
 #include "hash.h" /* /root/reference/afl_progs/hash.h (x86_64 hash32) */
 uint32_t REF_NAME(ref_hash32)(const void *key, uint32_t len, uint32_t seed) {
@@ -98,5 +116,5 @@ unsigned long long REF_NAME(ref_xxh64)(const void *input, size_t len, unsigned l
 }
 unsigned REF_NAME(ref_xxh_version)(void) { return XXH_versionNumber(); }
 #else
-#error "select one of REF_AFL / REF_DR / REF_HASH / REF_HASH_IGNORE / REF_XXH"
+#error "select one of REF_AFL / REF_DR / REF_PICKER / REF_HASH / REF_HASH_IGNORE / REF_XXH"
 #endif

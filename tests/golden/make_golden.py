@@ -165,10 +165,45 @@ def main():
                         s_map=sk.astype(np.uint8), s_idx=si.astype(np.uint32),
                         s_val=states[sj, sk, si], m_map=aj.astype(np.uint8),
                         m_idx=ai.astype(np.uint32), m_val=acc[aj, ai])
+    picker_fixture(R)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))
 
 
+def picker_fixture(R):
+    """5. picker ignore-bytes diff (picker/main.c:240-262), run by the reference's own loop:
+    3 files x 5 iterations x 4096 B; per file a sparse base trace, per iteration ~20 noisy
+    bytes, iteration 3 of file 1 identical to iteration 2 (a zero pair count)."""
+    rng = np.random.default_rng(0x91C4)
+    F, I, S = 3, 5, 4096
+    runs = np.zeros((F, I, S), np.uint8)
+    for f in range(F):
+        base = np.zeros(S, np.uint8)
+        idx = rng.choice(S, size=200, replace=False)
+        base[idx] = rng.integers(1, 256, size=200)
+        for it in range(I):
+            runs[f, it] = base
+            if f == 1 and it == 3:
+                runs[f, it] = runs[f, it - 1]
+                continue
+            noisy = rng.choice(S, size=20, replace=False)
+            runs[f, it, noisy] = rng.integers(0, 256, size=20)
+    ign = np.empty(S, np.uint8)
+    pc = np.zeros((F, I - 1), np.uint32)
+    tot = R.ref_picker_ignore_ref(P(runs), F, I, S, P(ign), P(pc))
+    rf, ri, rs = np.nonzero(runs)
+    np.savez_compressed(os.path.join(OUT, "picker.npz"), shape=np.array([F, I, S], np.uint32),
+                        r_file=rf.astype(np.uint8), r_iter=ri.astype(np.uint8),
+                        r_idx=rs.astype(np.uint32), r_val=runs[rf, ri, rs],
+                        ign_zero=np.nonzero(ign == 0)[0].astype(np.uint32),
+                        ign_other=np.array(sorted(set(ign.tolist()) - {0}), np.uint8),
+                        pair_counts=pc, total=np.array(tot, np.int64))
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["picker"]:
+        oracle.build()
+        picker_fixture(oracle.ref())
+    else:
+        main()

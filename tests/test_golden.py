@@ -157,3 +157,38 @@ def test_merge_gpu(gpu):
     got = merge_and(torch.from_numpy(st.reshape(5, -1)).cuda())
     torch.cuda.synchronize()
     np.testing.assert_array_equal(got.cpu().numpy().reshape(3, -1), exp)
+
+
+# ---- picker ignore-bytes diff (picker/main.c:240-262) ----------------------------------------
+
+def _picker_fixture():
+    f = load("picker.npz")
+    F, I, S = (int(x) for x in f["shape"])
+    runs = np.zeros((F, I, S), np.uint8)
+    runs[f["r_file"], f["r_iter"], f["r_idx"]] = f["r_val"]
+    ign = np.full(S, 0xFF, np.uint8)
+    ign[f["ign_zero"]] = 0
+    assert list(f["ign_other"]) == [0xFF]
+    return runs, ign, f["pair_counts"], int(f["total"])
+
+
+def test_picker_oracle(oracle_lib):
+    runs, ign, pc, tot = _picker_fixture()
+    g_ign, g_pc, g_tot = oracle.picker_ignore(runs)
+    np.testing.assert_array_equal(g_ign, ign)
+    np.testing.assert_array_equal(g_pc, pc)
+    assert g_tot == tot
+
+
+@pytest.mark.gpu
+def test_picker_gpu(gpu):
+    import torch
+
+    from killerbeez_amd.triage import picker_ignore
+
+    runs, ign, pc, tot = _picker_fixture()
+    g_ign, g_pc, g_tot = picker_ignore(torch.from_numpy(runs).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(g_ign.cpu().numpy(), ign)
+    np.testing.assert_array_equal(g_pc.cpu().numpy().view(np.uint32), pc)
+    assert int(g_tot.item()) == tot

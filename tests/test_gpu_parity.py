@@ -359,3 +359,73 @@ def test_ingest_ring(gpu, mode):
     if mode == MODE_DYNAMORIO:
         assert ctx.last_hash == exp["last_hash"]
     ctx.close()
+
+
+@pytest.mark.parametrize("files,iters,size", [(3, 7, 65536), (1, 2, 1 << 20), (2, 1, 4096),
+                                              (0, 4, 4096), (70000, 2, 16)])
+def test_picker_ignore(gpu, files, iters, size):
+    """kbz_picker_ignore_device vs the restated picker diff (picker/main.c:240-262)."""
+    import torch
+
+    from killerbeez_amd.triage import picker_ignore
+
+    rng = np.random.default_rng(files + 31 * iters)
+    base = rng.integers(0, 256, size=(files, 1, size), dtype=np.uint8)
+    runs = np.repeat(base, iters, axis=1)
+    noise = rng.random((files, iters, size)) < 0.005
+    runs[noise] = rng.integers(0, 256, size=int(noise.sum()), dtype=np.uint8)
+    ign, pc, tot = oracle.picker_ignore(runs)
+    g_ign, g_pc, g_tot = picker_ignore(torch.from_numpy(runs).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(g_ign.cpu().numpy(), ign)
+    np.testing.assert_array_equal(g_pc.cpu().numpy().view(np.uint32), pc)
+    assert int(g_tot.item()) == tot
+
+
+def test_picker_rejects_unaligned_size(gpu):
+    import torch
+
+    from killerbeez_amd.triage import picker_ignore
+
+    with pytest.raises(Exception):
+        picker_ignore(torch.zeros((1, 2, 24), dtype=torch.uint8, device="cuda"))
+
+
+def test_triage_modules_per_module_coverage(gpu):
+    """kbz_triage_modules_device = has_new_coverage_per_module (dynamorio_instrumentation.c:
+    1477-1493): every module keeps its own virgin map / ignore bytes / last hash; the per-exec
+    result is the OR over modules.  Two carried batches, 3 modules of different map sizes packed
+    in one row, ignore bytes on one module, repeated execs (last-hash skips)."""
+    import torch
+
+    from killerbeez_amd.triage import triage_modules
+
+    sizes = [65536, 4096, 16384]
+    offs = [0, 65536, 65536 + 4096]
+    row = sum(sizes)
+    rng = np.random.default_rng(1477)
+    ign = np.where(rng.random(4096) < 0.1, 0, 0xFF).astype(np.uint8)
+    ctxs = [TriageContext(m, MODE_DYNAMORIO, 300) for m in sizes]
+    ctxs[1].set_ignore(ign)
+    virgins = [np.full((3, m), 0xFF, np.uint8) for m in sizes]
+    lasts = [0] * 3
+    for b in range(2):
+        n = 300 - 100 * b
+        parts = [synth.sparse_np(n, m, seed=10 * b + i)[0] for i, m in enumerate(sizes)]
+        for p in parts:
+            p[50:60] = p[49]  # identical consecutive execs
+        traces = np.concatenate(parts, axis=1)
+        hnb, anyv = triage_modules(ctxs, torch.from_numpy(traces).cuda(), offs)
+        torch.cuda.synchronize()
+        exp_any = np.zeros(n, np.uint8)
+        for i, m in enumerate(sizes):
+            exp = oracle.triage_batch(MODE_DYNAMORIO, parts[i], None, virgin=virgins[i],
+                                      ignore=ign if i == 1 else None, last_hash=lasts[i])
+            np.testing.assert_array_equal(hnb[i].cpu().numpy(), exp["hnb"])
+            np.testing.assert_array_equal(ctxs[i].get_virgin(), exp["virgin"])
+            assert ctxs[i].last_hash == exp["last_hash"]
+            virgins[i], lasts[i] = exp["virgin"], exp["last_hash"]
+            exp_any |= (exp["hnb"] != 0).astype(np.uint8)
+        np.testing.assert_array_equal(anyv.cpu().numpy(), exp_any)
+    for c in ctxs:
+        c.close()

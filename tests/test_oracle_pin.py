@@ -194,3 +194,22 @@ def test_batch_triage_dynamorio_ignore(R):
         assert np.array_equal(r["hnb"], hnb)
         assert np.array_equal(r["virgin"][0], V[0])
         assert r["last_hash"] == last
+
+
+@pytest.mark.parametrize("files,iters,size", [(4, 6, 65536), (2, 1, 4096), (0, 3, 256),
+                                              (1, 2, 1 << 20)])
+def test_picker_ignore(R, files, iters, size):
+    """Restated picker diff vs the reference's own loop (picker/main.c:240-262)."""
+    rng = np.random.default_rng(files * 100 + iters)
+    base = rng.integers(0, 256, size=(files, 1, size), dtype=np.uint8)
+    runs = np.repeat(base, iters, axis=1)
+    noise = rng.random((files, iters, size)) < 0.01
+    runs[noise] = rng.integers(0, 256, size=int(noise.sum()), dtype=np.uint8)
+    ign, pc, tot = oracle.picker_ignore(runs)
+    r_ign = np.empty(size, np.uint8)
+    r_pc = np.zeros((files, max(iters - 1, 0)), np.uint32)
+    r_tot = R.ref_picker_ignore_ref(P(runs), files, iters, size, P(r_ign),
+                                    P(r_pc) if r_pc.size else None)
+    np.testing.assert_array_equal(ign, r_ign)
+    np.testing.assert_array_equal(pc, r_pc)
+    assert tot == r_tot
