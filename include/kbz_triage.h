@@ -231,6 +231,11 @@ int kbz_set_size(kbz_set_t *set, size_t *out);
 /* The first min(cap, size) keys in insertion order into host uint64[2*cap]; *n_out = size.
  * Synchronous. */
 int kbz_set_keys(kbz_set_t *set, uint64_t *host_out, size_t cap, size_t *n_out);
+/* A new set holding the union of two sets, replacing linux_ipt_merge
+ * (linux_ipt_instrumentation.c:944-978): first's keys in first's insertion order, then the keys
+ * of second absent from first, in second's insertion order.  Neither input is changed.  Runs on
+ * the device, ordered on `stream`; NULL on failure (kbz_set_last_error). */
+kbz_set_t *kbz_set_merge(kbz_set_t *first, kbz_set_t *second, void *stream);
 
 #ifdef __cplusplus
 }

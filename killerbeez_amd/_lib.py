@@ -52,6 +52,7 @@ SIGNATURES = [
     ("kbz_set_insert_device", _i, [_vp, _vp, _vp, _sz, _vp, _vp]),
     ("kbz_set_size", _i, [_vp, C.POINTER(_sz)]),
     ("kbz_set_keys", _i, [_vp, _vp, _sz, C.POINTER(_sz)]),
+    ("kbz_set_merge", _vp, [_vp, _vp, _vp]),
 ]
 
 

@@ -110,6 +110,26 @@ __global__ void k_set_insert(Slot *tab, size_t mask, const unsigned long long *k
   atomicOr(overflow, 1u);
 }
 
+// Merge support: a table's slots in insertion order.  Sorting (seq, slot) puts occupied slots
+// first in the order they were inserted (free slots carry seq = kEmpty and sort last).
+__global__ void k_slot_seq(const Slot *tab, uint32_t nslots, unsigned long long *seq_out,
+                           uint32_t *idx_out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nslots) return;
+  seq_out[i] = tab[i].seq;
+  idx_out[i] = i;
+}
+
+__global__ void k_slot_gather(const Slot *tab, const uint32_t *idx, uint32_t nslots,
+                              unsigned long long *keys_out, uint8_t *mask_out) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nslots) return;
+  const Slot s = tab[idx[p]];
+  keys_out[2 * p] = s.lo;
+  keys_out[2 * p + 1] = s.hi;
+  mask_out[p] = s.seq != kEmpty;
+}
+
 thread_local std::string g_set_err;
 int set_fail(const std::string &m) {
   g_set_err = m;
@@ -205,6 +225,65 @@ int kbz_set_insert_device(kbz_set_t *s, const uint64_t *keys, const uint8_t *mas
   SET_TRY(hipFreeAsync(idx_out, st));
   SET_TRY(hipFreeAsync(tmp, st));
   return 0;
+}
+
+// Insert every key of src into dst, in src's insertion order (device-only, stream-ordered).
+static int append_set(kbz_set_t *dst, const kbz_set_t *src, hipStream_t st) {
+  const size_t nslots = src->mask + 1;
+  if (nslots > 0x7fffffffu) return set_fail("source table too large");
+  const unsigned blocks = (unsigned)((nslots + 255) / 256);
+  unsigned long long *seq_in = nullptr, *seq_out = nullptr, *keys = nullptr;
+  uint32_t *idx_in = nullptr, *idx_out = nullptr;
+  uint8_t *occupied = nullptr, *is_new = nullptr;
+  void *tmp = nullptr;
+  size_t tmp_bytes = 0;
+  SET_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, seq_in, seq_out, idx_in, idx_out,
+                                             (int)nslots, 0, 64, st));
+  SET_TRY(hipMallocAsync((void **)&seq_in, nslots * 8, st));
+  SET_TRY(hipMallocAsync((void **)&seq_out, nslots * 8, st));
+  SET_TRY(hipMallocAsync((void **)&idx_in, nslots * 4, st));
+  SET_TRY(hipMallocAsync((void **)&idx_out, nslots * 4, st));
+  SET_TRY(hipMallocAsync((void **)&keys, nslots * 16, st));
+  SET_TRY(hipMallocAsync((void **)&occupied, nslots, st));
+  SET_TRY(hipMallocAsync((void **)&is_new, nslots, st));
+  SET_TRY(hipMallocAsync(&tmp, tmp_bytes ? tmp_bytes : 1, st));
+  hipLaunchKernelGGL(k_slot_seq, dim3(blocks), dim3(256), 0, st, src->tab, (uint32_t)nslots,
+                     seq_in, idx_in);
+  SET_TRY(hipGetLastError());
+  SET_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, seq_in, seq_out, idx_in, idx_out,
+                                             (int)nslots, 0, 64, st));
+  hipLaunchKernelGGL(k_slot_gather, dim3(blocks), dim3(256), 0, st, src->tab, idx_out,
+                     (uint32_t)nslots, keys, occupied);
+  SET_TRY(hipGetLastError());
+  if (kbz_set_insert_device(dst, (const uint64_t *)keys, occupied, nslots, is_new, st)) return -1;
+  SET_TRY(hipFreeAsync(seq_in, st));
+  SET_TRY(hipFreeAsync(seq_out, st));
+  SET_TRY(hipFreeAsync(idx_in, st));
+  SET_TRY(hipFreeAsync(idx_out, st));
+  SET_TRY(hipFreeAsync(keys, st));
+  SET_TRY(hipFreeAsync(occupied, st));
+  SET_TRY(hipFreeAsync(is_new, st));
+  SET_TRY(hipFreeAsync(tmp, st));
+  return 0;
+}
+
+kbz_set_t *kbz_set_merge(kbz_set_t *first, kbz_set_t *second, void *stream) {
+  if (!first || !second) {
+    set_fail("null argument");
+    return nullptr;
+  }
+  // Each input holds at most slots/2 keys (kbz_set_create's load factor), so this fits both.
+  kbz_set_t *m = kbz_set_create((first->mask + 1 + second->mask + 1) / 2);
+  if (!m) return nullptr;
+  hipStream_t st = (hipStream_t)stream;
+  if (append_set(m, first, st) || append_set(m, second, st)) {
+    std::string err = g_set_err;
+    (void)hipStreamSynchronize(st);
+    kbz_set_destroy(m);
+    set_fail("kbz_set_merge: " + err);
+    return nullptr;
+  }
+  return m;
 }
 
 int kbz_set_size(kbz_set_t *s, size_t *out) {

@@ -387,6 +387,17 @@ class UniqueSet:
         self._check(lib().kbz_set_keys(self._h, _np_ptr(out), n, C.byref(got)), "kbz_set_keys")
         return out[:got.value]
 
+    def merge(self, other: "UniqueSet", stream=None) -> "UniqueSet":
+        """A new set: the union of self and other, self's keys first (linux_ipt_merge,
+        linux_ipt_instrumentation.c:944-978).  Neither input changes."""
+        L = lib()
+        h = L.kbz_set_merge(self._h, other._h, _stream_handle(stream))
+        if not h:
+            raise KbzError("kbz_set_merge: " + (L.kbz_set_last_error() or b"").decode())
+        m = UniqueSet.__new__(UniqueSet)
+        m._h = h
+        return m
+
 
 def dedup_keys(x64, outcome):
     """Keys {XXH64 of the transformed trace, outcome class} for UniqueSet (CUDA int64 [n, 2])."""

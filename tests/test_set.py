@@ -100,3 +100,45 @@ def test_unique_crashes_from_triage(gpu):
         got = s.insert(dedup_keys(out["x64"], to), to != 0).cpu().numpy()
     np.testing.assert_array_equal(got, exp_new[0])
     assert got[99] == 1 and not got[100:140].any()
+
+
+def reference_merge(first_keys, second_keys):
+    """linux_ipt_merge (linux_ipt_instrumentation.c:944-978): a fresh table, every entry of the
+    first state (HASH_ITER order = insertion order), then each entry of the second state that
+    HASH_FIND misses."""
+    seen = {}
+    for k in map(tuple, first_keys):
+        seen.setdefault(k, len(seen))
+    for k in map(tuple, second_keys):
+        if k not in seen:
+            seen[k] = len(seen)
+    return np.array(list(seen.keys()), np.uint64).reshape(-1, 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_a,n_b", [(700, 900), (0, 300), (300, 0), (1, 1)])
+def test_merge_like_linux_ipt_merge(gpu, n_a, n_b):
+    from killerbeez_amd.triage import UniqueSet
+
+    rng = np.random.default_rng(n_a * 7 + n_b)
+    pool = rng.integers(0, 2**63, size=(500, 2), dtype=np.uint64)
+    pool[3, 0] = pool[4, 0]  # same low word, different high word
+    a_rows = pool[rng.integers(0, 500, size=n_a)]
+    b_rows = pool[rng.integers(0, 500, size=n_b)]
+    a, b = UniqueSet(1024), UniqueSet(2048)
+    if n_a:
+        a.insert(_dev(a_rows))
+    if n_b:
+        b.insert(_dev(b_rows))
+    a_keys, b_keys = a.keys(), b.keys()
+    m = a.merge(b)
+    exp = reference_merge(a_keys, b_keys)
+    assert m.size() == len(exp)
+    np.testing.assert_array_equal(m.keys(), exp)
+    # inputs unchanged; the merged set keeps answering novelty like the reference's table
+    np.testing.assert_array_equal(a.keys(), a_keys)
+    np.testing.assert_array_equal(b.keys(), b_keys)
+    probe = np.concatenate([pool[:50], rng.integers(0, 2**63, size=(20, 2), dtype=np.uint64)])
+    got = m.insert(_dev(probe)).cpu().numpy()
+    exp_new, _ = reference_set([np.concatenate([exp, probe])])
+    np.testing.assert_array_equal(got, exp_new[0][len(exp):])
