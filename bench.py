@@ -203,10 +203,14 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     achieved = B * M / (pass1_ms * 1e-3) / 1e9  # GB/s, algorithmic bytes of one launch
     traffic = None
-    tf = os.path.join(ROOT, "profiles", "pass1_traffic.json")
+    # PMC bytes per launch measured for THIS workload's pass-1 kernel (scripts/pmc_traffic.py)
+    tf = os.path.join(ROOT, "profiles", "pass1_traffic.json" if args.workload == "config2"
+                      else f"pass1_traffic_{args.workload}.json")
     if os.path.exists(tf):
         try:
-            traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
+            tj = json.load(open(tf))
+            if tj.get("workload", "config2") == args.workload:
+                traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     res = {
@@ -230,7 +234,7 @@ def main():
                    "mode": args.mode, "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": "k_pass1 (+2 tiny memsets)",
+                     "traffic": traffic, "kernel": ("k_pass1w" if args.workload == "config3" else "k_pass1s") + " (+2 tiny memsets)",
                      "avg_launch_ms": round(pass1_ms, 4),
                      "algorithmic_bytes_per_launch": B * M},
         "pass1_share_of_step": round(pass1_ms / ms_per_step, 4),
