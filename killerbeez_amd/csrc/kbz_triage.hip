@@ -1091,7 +1091,9 @@ __global__ __launch_bounds__(256) void k_or_reduce(uint8_t *out, const uint8_t *
 }
 
 // ---- merger: AND-fold -----------------------------------------------------------------------
-// partial[g][:] = AND of states in group g (16 B per thread, 4 independent loads in flight).
+// partial[g][:] = AND of states in group g (16 B per thread, 8 independent streaming loads in
+// flight; states are read once, so the loads bypass cache retention).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void k_and_groups(const uint8_t *states, size_t n,
                                                      size_t state_bytes, size_t group_len,
                                                      uint8_t *partial) {
@@ -1099,23 +1101,19 @@ __global__ __launch_bounds__(256) void k_and_groups(const uint8_t *states, size_
   const size_t g = blockIdx.y;
   if (col >= state_bytes) return;
   const size_t s0 = g * group_len, s1 = std::min(n, s0 + group_len);
-  uint4 acc = make_uint4(~0u, ~0u, ~0u, ~0u);
+  const u32x4 *p = (const u32x4 *)(states + col);
+  const size_t st = state_bytes / 16;  // row stride in u32x4
+  u32x4 acc = {~0u, ~0u, ~0u, ~0u};
   size_t s = s0;
-  for (; s + 4 <= s1; s += 4) {
-    const uint4 a = *(const uint4 *)(states + s * state_bytes + col);
-    const uint4 b = *(const uint4 *)(states + (s + 1) * state_bytes + col);
-    const uint4 c = *(const uint4 *)(states + (s + 2) * state_bytes + col);
-    const uint4 d = *(const uint4 *)(states + (s + 3) * state_bytes + col);
-    acc.x &= a.x & b.x & c.x & d.x;
-    acc.y &= a.y & b.y & c.y & d.y;
-    acc.z &= a.z & b.z & c.z & d.z;
-    acc.w &= a.w & b.w & c.w & d.w;
+  for (; s + 8 <= s1; s += 8) {
+    u32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[u] = __builtin_nontemporal_load(p + (s + u) * st);
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc &= v[u];
   }
-  for (; s < s1; s++) {
-    const uint4 a = *(const uint4 *)(states + s * state_bytes + col);
-    acc.x &= a.x; acc.y &= a.y; acc.z &= a.z; acc.w &= a.w;
-  }
-  *(uint4 *)(partial + g * state_bytes + col) = acc;
+  for (; s < s1; s++) acc &= __builtin_nontemporal_load(p + s * st);
+  *(u32x4 *)(partial + g * state_bytes + col) = acc;
 }
 __global__ __launch_bounds__(256) void k_and_rows(const uint8_t *rows, size_t nrows, size_t bytes,
                                                    uint8_t *out, int accumulate) {
@@ -1999,12 +1997,32 @@ int kbz_merge_and_device(uint8_t *out, const uint8_t *states, size_t n, size_t s
   }
   const size_t glen = (n + groups - 1) / groups;
   groups = (n + glen - 1) / glen;
+  // Tree: stage 1 folds groups of glen states; later stages fold 16 partial rows per group
+  // (a full-width grid each) until at most 16 rows are left for k_and_rows, whose one thread per
+  // column would otherwise walk every partial row with dependent round trips.
+  constexpr size_t kTreeLen = 16;
+  size_t total_rows = groups;
+  for (size_t r = groups; r > kTreeLen;) {
+    r = (r + kTreeLen - 1) / kTreeLen;
+    total_rows += r;
+  }
   uint8_t *partial = nullptr;
-  HIP_TRY(hipMallocAsync((void **)&partial, groups * state_bytes, s));
+  HIP_TRY(hipMallocAsync((void **)&partial, total_rows * state_bytes, s));
   hipLaunchKernelGGL(k_and_groups, dim3(gx, (unsigned)groups), dim3(256), 0, s, states, n,
                      state_bytes, glen, partial);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_and_rows, dim3(gx), dim3(256), 0, s, partial, groups, state_bytes, out, 0);
+  uint8_t *src = partial;
+  size_t rows = groups;
+  while (rows > kTreeLen) {
+    const size_t next = (rows + kTreeLen - 1) / kTreeLen;
+    uint8_t *dst = src + rows * state_bytes;
+    hipLaunchKernelGGL(k_and_groups, dim3(gx, (unsigned)next), dim3(256), 0, s, src, rows,
+                       state_bytes, kTreeLen, dst);
+    HIP_TRY(hipGetLastError());
+    src = dst;
+    rows = next;
+  }
+  hipLaunchKernelGGL(k_and_rows, dim3(gx), dim3(256), 0, s, src, rows, state_bytes, out, 0);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipFreeAsync(partial, s));
   return 0;

@@ -210,6 +210,22 @@ def test_merge_states_property(gpu):
     np.testing.assert_array_equal(got, np.bitwise_and.reduce(s, axis=0))
 
 
+@pytest.mark.parametrize("n,nbytes", [(5000, 4096), (3000, 3 * 65536)])
+def test_merge_tree_sparse_clears(gpu, n, nbytes):
+    """Enough states for the multi-stage fold tree (5000 x 4 KiB: 312 -> 20 -> 2 partial rows);
+    about nbytes*8 bits cleared over all states, so the AND keeps ~1/3 of its bits set."""
+    import torch
+
+    rng = np.random.default_rng(n)
+    s = np.full((n, nbytes), 0xFF, np.uint8)
+    pos = rng.integers(0, n * nbytes * 8, size=nbytes * 8)
+    np.bitwise_and.at(s.reshape(-1), pos // 8, ~(np.uint8(1) << (pos % 8).astype(np.uint8)))
+    exp = np.bitwise_and.reduce(s, axis=0)
+    assert 0.2 < np.unpackbits(exp).mean() < 0.6
+    got = merge_and(torch.from_numpy(s).cuda()).cpu().numpy()
+    np.testing.assert_array_equal(got, exp)
+
+
 @pytest.mark.parametrize("length", [8, 64, 256, 4096, 65536])
 def test_row_hashes(gpu, length):
     import torch
