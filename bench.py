@@ -234,7 +234,7 @@ def main():
                    "mode": args.mode, "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": ("k_pass1w" if args.workload == "config3" else "k_pass1s") + " (+2 tiny memsets)",
+                     "traffic": traffic, "kernel": ("k_pass1w" if args.workload == "config3" else "k_pass1s"),
                      "avg_launch_ms": round(pass1_ms, 4),
                      "algorithmic_bytes_per_launch": B * M},
         "pass1_share_of_step": round(pass1_ms / ms_per_step, 4),
