@@ -169,7 +169,7 @@ def main():
             if record:
                 ev[1].record()
                 timings.append(ev)
-            ctx.shard_link(None, True, None)
+            ctx.shard_link(None, None, True, None, None)
             ctx.shard_reduce()
             ctx.shard_finish(None, None)  # single shard: its own aggregate is the total
         else:

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define KBZ_ABI_VERSION 1
+#define KBZ_ABI_VERSION 2
 
 /* Triage semantics (which reference code path a batch reproduces). */
 enum kbz_mode {
@@ -85,12 +85,24 @@ int kbz_set_ignore(kbz_ctx_t *ctx, const uint8_t *host_ignore);
  * virgin_crash.  DYNAMORIO mode uses only virgin_bits.  Synchronous. */
 int kbz_get_virgin(kbz_ctx_t *ctx, uint8_t *host_out);
 int kbz_set_virgin(kbz_ctx_t *ctx, const uint8_t *host_in);
-/* DynamoRIO last_shm_hash (dynamorio_instrumentation.c:1450-1461).  Synchronous. */
+/* DynamoRIO last_shm_hash (dynamorio_instrumentation.c:1450-1461).  Synchronous.  The context
+ * also keeps the previous batch's last trace (to tell a repeated exec from a hash collision);
+ * kbz_set_last_hash forgets it, so a restored hash is handled without it (still exact). */
 int kbz_get_last_hash(kbz_ctx_t *ctx, uint32_t *out);
 int kbz_set_last_hash(kbz_ctx_t *ctx, uint32_t value);
 /* Device pointer to the current virgin maps (3*map_size bytes); valid until the next triage
  * call (the context double-buffers them). */
 uint8_t *kbz_virgin_device(kbz_ctx_t *ctx);
+
+/* Which pass-1 kernel triages a batch: AUTO picks by batch shape (the wide-map variant when a
+ * batch has fewer than 512 chunks of 64 traces, i.e. fewer than two per CU); NARROW / WIDE force
+ * one (tests run every parity case through both; results are identical).  Default AUTO. */
+enum kbz_pass1 { KBZ_PASS1_AUTO = 0, KBZ_PASS1_NARROW = 1, KBZ_PASS1_WIDE = 2 };
+int kbz_ctx_set_pass1(kbz_ctx_t *ctx, int choice);
+/* Work counters of the last finished batch, host uint32 out[3]: claim items resolved (new
+ * coverage found), chunks recomputed by the DynamoRIO skip fix path, DynamoRIO skipped rows that
+ * differ from their predecessor (hash collisions).  Synchronous; diagnostics only. */
+int kbz_ctx_stats(kbz_ctx_t *ctx, uint32_t *out);
 
 /* ---- batched triage ------------------------------------------------------------------------ */
 /* traces:   device, n rows of map_size raw 8-bit hit counters, row j at traces + j*stride
@@ -133,9 +145,10 @@ int kbz_ring_flush(kbz_ctx_t *ctx);
 /* A batch split into contiguous shards, one per GPU (rank g holds traces [lo_g, hi_g)), gives
  * the same results as one kbz_triage_batch over the whole batch when each rank runs:
  *   1. kbz_shard_begin(ctx, shard, ...)                 -- local streaming pass
- *   2. all-gather of kbz_shard_last_hash (DYNAMORIO only), then kbz_shard_link(ctx, prev_last,
- *      is_first_shard, global_last) with prev_last = pair of the nearest non-empty earlier
- *      rank and global_last = pair of the last non-empty rank
+ *   2. (DYNAMORIO only) all-gather of kbz_shard_last_hash and kbz_shard_last_row, then
+ *      kbz_shard_link(ctx, prev_last, prev_row, is_first_shard, global_last, global_row) with
+ *      prev_* = pair / row of the nearest non-empty earlier rank and global_* = pair / row of
+ *      the last non-empty rank (other modes: kbz_shard_link(ctx, NULL, NULL, 1, NULL, NULL))
  *   3. kbz_shard_reduce(ctx)                            -- local OR aggregates
  *   4. all-gather of kbz_shard_aggregate (nclass*map_size bytes per rank, device memory),
  *      OR of the ranks before this one -> prefix, OR of all ranks -> total
@@ -147,10 +160,17 @@ int kbz_shard_begin(kbz_ctx_t *ctx, const uint8_t *traces, size_t n, size_t stri
                     void *stream);
 /* Copies {h32 of this shard's last trace, n != 0} into device uint32 d_out[2]. */
 int kbz_shard_last_hash(kbz_ctx_t *ctx, uint32_t *d_out, void *stream);
-/* prev_last: device uint32[2] from the previous rank (ignored when is_first); global_last:
- * device uint32[2] from the last non-empty rank (becomes the context's last hash). */
-int kbz_shard_link(kbz_ctx_t *ctx, const uint32_t *prev_last, int is_first,
-                   const uint32_t *global_last, void *stream);
+/* Copies this shard's last raw trace (map_size bytes) into device d_out; nothing for an empty
+ * shard. */
+int kbz_shard_last_row(kbz_ctx_t *ctx, uint8_t *d_out, void *stream);
+/* prev_last: device uint32[2] from the previous rank (ignored when is_first); prev_row: device
+ * map_size bytes, that rank's last raw trace, or NULL (unknown: exact, slower if it repeats).
+ * global_last: device uint32[2] from the last non-empty rank (becomes the context's last hash)
+ * or NULL = this shard's own (a single-shard batch); global_row: that rank's last raw trace
+ * (remembered as the next batch's row-0 predecessor) or NULL. */
+int kbz_shard_link(kbz_ctx_t *ctx, const uint32_t *prev_last, const uint8_t *prev_row,
+                   int is_first, const uint32_t *global_last, const uint8_t *global_row,
+                   void *stream);
 int kbz_shard_reduce(kbz_ctx_t *ctx, void *stream);
 /* Copies this shard's OR aggregate (nclass*map_size bytes; nclass = 1 in DYNAMORIO mode,
  * 3 otherwise) into device memory d_out.  Only bits still virgin at batch entry are kept (the

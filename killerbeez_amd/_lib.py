@@ -12,6 +12,7 @@ import re
 from . import build as _build
 
 _LIB = None
+ABI_VERSION = 2
 
 # (name, restype, argtypes) for every function declared in include/kbz_triage.h
 _vp, _sz, _i, _u32, _u64 = C.c_void_p, C.c_size_t, C.c_int, C.c_uint32, C.c_uint64
@@ -26,6 +27,8 @@ SIGNATURES = [
     ("kbz_get_last_hash", _i, [_vp, C.POINTER(_u32)]),
     ("kbz_set_last_hash", _i, [_vp, _u32]),
     ("kbz_virgin_device", _vp, [_vp]),
+    ("kbz_ctx_set_pass1", _i, [_vp, _i]),
+    ("kbz_ctx_stats", _i, [_vp, _vp]),
     ("kbz_triage_batch_device", _i, [_vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _i, _vp]),
     ("kbz_triage_batch_host", _i, [_vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _i]),
     ("kbz_ring_acquire", _i, [_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_sz)]),
@@ -33,7 +36,8 @@ SIGNATURES = [
     ("kbz_ring_flush", _i, [_vp]),
     ("kbz_shard_begin", _i, [_vp, _vp, _sz, _sz, _vp, _vp, _vp, _i, _vp]),
     ("kbz_shard_last_hash", _i, [_vp, _vp, _vp]),
-    ("kbz_shard_link", _i, [_vp, _vp, _i, _vp, _vp]),
+    ("kbz_shard_last_row", _i, [_vp, _vp, _vp]),
+    ("kbz_shard_link", _i, [_vp, _vp, _vp, _i, _vp, _vp, _vp]),
     ("kbz_shard_reduce", _i, [_vp, _vp]),
     ("kbz_shard_aggregate", _i, [_vp, _vp, _vp]),
     ("kbz_shard_aggregate_bytes", _sz, [_vp]),
@@ -84,7 +88,7 @@ def lib(build_if_missing: bool = True):
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.kbz_abi_version() != 1:
+    if L.kbz_abi_version() != ABI_VERSION:
         raise KbzError("ABI version mismatch")
     _LIB = L
     return L

@@ -57,7 +57,7 @@ __device__ __forceinline__ size_t home(unsigned long long lo, unsigned long long
 
 __global__ void k_set_probe(const Slot *tab, size_t mask, const unsigned long long *keys,
                             const uint8_t *in_mask, uint32_t n, unsigned long long *sort_lo,
-                            uint32_t *sort_idx, uint8_t *is_new) {
+                            uint32_t *sort_idx, uint8_t *is_new, uint32_t *overflow) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   sort_idx[j] = j;
@@ -74,6 +74,9 @@ __global__ void k_set_probe(const Slot *tab, size_t mask, const unsigned long lo
     }
     if (s.lo == lo && s.hi == hi) return;  // already in the set
   }
+  // every slot taken and none holds the key: it is new but cannot be inserted -- report it
+  // (kbz_set_size fails) rather than calling it already seen
+  atomicOr(overflow, 1u);
 }
 
 __global__ void k_set_first(const unsigned long long *s_lo, const uint32_t *s_idx, uint32_t n,
@@ -208,7 +211,7 @@ int kbz_set_insert_device(kbz_set_t *s, const uint64_t *keys, const uint8_t *mas
   SET_TRY(hipMallocAsync((void **)&idx_out, n * 4, st));
   SET_TRY(hipMallocAsync(&tmp, tmp_bytes ? tmp_bytes : 1, st));
   hipLaunchKernelGGL(k_set_probe, dim3(blocks), dim3(256), 0, st, s->tab, s->mask, k, mask,
-                     (uint32_t)n, lo_in, idx_in, is_new_out);
+                     (uint32_t)n, lo_in, idx_in, is_new_out, s->overflow);
   SET_TRY(hipGetLastError());
   SET_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, lo_in, lo_out, idx_in, idx_out,
                                              (int)n, 0, 64, st));

@@ -124,6 +124,13 @@ __device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[4]) {
                : "memory");
 }
 template <int N>
+__device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[5]) {
+  asm volatile("s_waitcnt vmcnt(%5)"
+               : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4])
+               : "n"(N)
+               : "memory");
+}
+template <int N>
 __device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[8]) {
   asm volatile("s_waitcnt vmcnt(%8)"
                : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
@@ -398,22 +405,30 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
     const uint32_t seg = chunk / a.seg_len;
     // Virgin words of each tile travel with its rows: a 9th ring register per slot (lane l < 16 NC
     // loads 16 B of class l / 16), stored to a per-buffer LDS area next to the tile, so T can
-    // limit its stores to words that still hold virgin bits (below).
+    // limit its stores to words that still hold virgin bits (below).  DynamoRIO (NC = 1): lanes
+    // 16-31 load the tile's 256 B of the PREVIOUS chunk's last row into the same area, so row 0
+    // (lane 0, which has no predecessor inside the wave) gets an exact neighbour test too.
+    // Chunk 0 has no previous row here (its row 0 is compared with the previous batch's or
+    // shard's last row by k_skip); it re-loads its own row 0 and ignores it.
     u32x4 R[D][NLD + 1];
+    constexpr int NXL = (MODE == KBZ_MODE_DYNAMORIO) ? 32 : 16 * NC;  // lanes with a 9th load
     const uint32_t vl = min(lane, 16 * NC - 1);
-    const uint8_t *vbase = a.vcur + (size_t)(vl / 16) * a.map_size + (vl % 16) * 16;
+    const uint8_t *xbase = a.vcur + (size_t)(vl / 16) * a.map_size + (vl % 16) * 16;
+    if (MODE == KBZ_MODE_DYNAMORIO && lane >= 16 && lane < 32)
+      xbase = a.traces + (row0 ? row0 - 1 : 0) * a.stride + (lane - 16) * 16;
     auto load_t = [&](u32x4 (&r)[NLD + 1], uint32_t t) {
       load_half(*(u32x4(*)[NLD])r, t);
       const uint32_t msk = t < ntiles ? ~0u : 0u;
-      asm_load16_cached(r[NLD], vbase + ((t * TW) & msk));
+      asm_load16_cached(r[NLD], xbase + ((t * TW) & msk));
     };
     auto store_t = [&](const u32x4 (&r)[NLD + 1], int b) {
       store_half(*(const u32x4(*)[NLD])r, b);
-      if (lane < 16 * NC) {
+      if (lane < NXL) {
         const u32x4 v = r[NLD];
         lds[2 * TILE + b * 48 + lane] = make_uint4(v.x, v.y, v.z, v.w);
       }
     };
+    bool neq0 = false;  // DynamoRIO, chunk > 0: row 0 differs from the previous chunk's last row
 #pragma unroll
     for (int d = 0; d < D; d++) load_t(R[d], d);
     uint64_t tfl[NC];  // stored-tile bits of the current 64-tile flag word
@@ -464,6 +479,17 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         // raw AFL words are their own transform (only simplified lanes change)
         if (dirty && (MODE != KBZ_MODE_AFL || simp)) *slot = v;
       }
+      if (MODE == KBZ_MODE_DYNAMORIO && chunk > 0 && !(ABL & 1)) {
+        // row 0 (transformed in place above; all-zero columns stay 0 == classify(0)) against
+        // the previous chunk's last row, word `lane` of this tile, on the examined bytes
+        uint64_t d = 0;
+        if (lane < TW / 8) {
+          const uint64_t pw = classify8(((const uint64_t *)&lds[2 * TILE + b * 48 + 16])[lane]);
+          const uint64_t cw = ((const uint64_t *)&lds[b * TILE + (lane >> 1)])[lane & 1];
+          d = (pw ^ cw) & (IGN ? ~nonzero_bytes8(ig[lane]) : ~0ull);
+        }
+        neq0 |= __ballot(d != 0) != 0;
+      }
       // chunk_or keeps only bits still virgin at batch entry (orw & V): the scan uses nothing
       // else (its new bits are o & V & ~prev, and f2 only looks at bytes with V == 0xff), and a
       // tile with none is not stored at all, only its flag bit stays clear.  In steady-state
@@ -510,7 +536,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
     }
     KBZ_STAMP_FLUSH(chunk * 2 + 1);
     drain_asm_loads(R);
-    if (MODE == KBZ_MODE_DYNAMORIO && valid) a.neq[row0 + lane] = neq != 0;
+    if (MODE == KBZ_MODE_DYNAMORIO && valid) a.neq[row0 + lane] = (lane == 0 && chunk > 0) ? neq0 : neq != 0;
   }
 }
 
@@ -545,12 +571,14 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
   static_assert(kChunk % (2 * NX) == 0, "equal row groups");
   constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, RPW = kChunk / NL, NLD = RPW / RPI;
+  constexpr int NE = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 0;  // extra loads per tile (prev row)
   constexpr int TILE = kChunk * SLOTS;  // uint4 per tile buffer
   constexpr int RG = kChunk / (2 * NX);  // rows per X row group
   __shared__ uint4 lds[3 * TILE];
   __shared__ uint4 kbuf[3 * TILE];             // k of each (row, word), same layout as lds
   __shared__ uint64_t orb[3][NC][TW / 8];      // column ORs of the tile, per class
   __shared__ uint64_t bnd[2][2 * NX][TW / 8];  // last row of each group (neighbour test)
+  __shared__ uint64_t prv[3][TW / 8];          // DynamoRIO: previous chunk's last row, raw
   __shared__ uint64_t neqs[NX];
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -579,17 +607,27 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
 #pragma unroll
     for (int i = 0; i < NLD; i++)
       roff[i] = (uint32_t)(min(RPW * li + RPI * i + lr, nrows - 1) * a.stride);
-    auto load_half = [&](u32x4 (&r)[NLD], uint32_t t) {  // branch-free (see k_pass1s)
+    // DynamoRIO: one more load per tile, the previous chunk's last row (loader 0, lanes 0-15:
+    // 16 B each; every other lane repeats lane 0's address), for row 0's neighbour test.  Chunk
+    // 0 re-loads its own row 0 and ignores it (k_skip compares it across batches / shards).
+    const uint8_t *pbase = a.traces + (row0 ? row0 - 1 : 0) * a.stride +
+                           ((li == 0 && lane < SLOTS) ? lane * 16 : 0);
+    auto load_half = [&](u32x4 (&r)[NLD + NE], uint32_t t) {  // branch-free (see k_pass1s)
       const uint32_t msk = t < ntiles ? ~0u : 0u;
 #pragma unroll
       for (int i = 0; i < NLD; i++) asm_load16(r[i], lbase + ((t * TW + roff[i]) & msk));
+      if (NE) asm_load16_cached(r[NLD + NE - 1], pbase + ((t * TW) & msk));
     };
-    auto store_half = [&](const u32x4 (&r)[NLD], int b) {
+    auto store_half = [&](const u32x4 (&r)[NLD + NE], int b) {
 #pragma unroll
       for (int i = 0; i < NLD; i++) {
         const int rr = RPW * li + RPI * i + lr;
         const u32x4 v = r[i];
         lds[b * TILE + rr * SLOTS + (ls ^ (rr & 15))] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      if (NE && li == 0 && lane < SLOTS) {
+        const u32x4 v = r[NLD + NE - 1];
+        ((uint4 *)&prv[b][0])[lane] = make_uint4(v.x, v.y, v.z, v.w);
       }
     };
     uint64_t h = (uint64_t)(kHashConst ^ a.map_size);
@@ -619,7 +657,7 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
       }
     };
     if (isLd) {  // the whole ring lives inside this wave-uniform branch
-      u32x4 R[D][NLD];
+      u32x4 R[D][NLD + NE];
 #pragma unroll
       for (int d = 0; d < D; d++) load_half(R[d], d);
       for (uint32_t g = 0; g < nsteps; g += D) {
@@ -629,7 +667,7 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
 #ifndef KBZ_XP_NOCHAIN
           if (isL && s >= 2 && s - 2 < ntiles) chain_tile(s - 2);
 #endif
-          vmcnt_wait_ring<(D - 1) * NLD>(R[u]);
+          vmcnt_wait_ring<(D - 1) * (NLD + NE)>(R[u]);
           store_half(R[u], s % 3);
           load_half(R[u], s + D);
           lds_barrier();
@@ -689,8 +727,7 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
       for (int k = 0; k < NC; k++) c = ((present[k] >> (r0 + i)) & 1) ? (uint32_t)k : c;
       clsw |= c << (2 * i);
     }
-    if (xi == 0) {  // every tile of chunk_or is stored (unmasked) here: all flags set
-      for (uint32_t i = lane; i < NC * a.nfw; i += 64) a.tflags[(size_t)chunk * NC * a.nfw + i] = ~0ull;
+    if (xi == 0) {
       if (lane == 0) {
         uint8_t m = 0;
 #pragma unroll
@@ -757,25 +794,44 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
     };
     // one step after tile t was transformed: group-boundary neighbour test, and X_0 stores
     // the tile's column ORs
+    uint64_t tfl[NC];  // X_0: stored-tile bits of the current 64-tile flag word (k_pass1s)
+#pragma unroll
+    for (int k = 0; k < NC; k++) tfl[k] = 0;
+    uint64_t *tfbase = a.tflags + (size_t)chunk * NC * a.nfw;
     auto finish_tile = [&](uint32_t t) {
       if (MODE == KBZ_MODE_DYNAMORIO) {
-        const uint64_t pl = grp > 0 ? bnd[t & 1][grp - 1][w] : 0;  // row 0: against 0
+        // group 0's first row is row 0: against the previous chunk's last row (chunk 0: 0, a
+        // placeholder k_skip does not use)
+        const uint64_t pl = grp > 0 ? bnd[t & 1][grp - 1][w]
+                                    : (chunk > 0 ? classify8(prv[t % 3][w]) : 0);
         const uint64_t bal = __ballot(((ftw ^ pl) & frel) != 0);
         nm |= ((uint64_t)((uint32_t)bal != 0) << r0a) |
               ((uint64_t)((uint32_t)(bal >> 32) != 0) << r0b);
       }
-      if (xi == 0 && lane < TW / 8) {
+      if (xi == 0) {
+        // like k_pass1s: chunk_or and the segment aggregate keep only the bits still virgin at
+        // batch entry; a tile with none is not stored, its flag bit stays clear
         const int b = t % 3;
 #pragma unroll
         for (int k = 0; k < NC; k++) {
           if (!present[k]) continue;
-          const uint64_t o = orb[b][k][lane];
-          orb[b][k][lane] = 0;
-          const size_t off = (size_t)k * a.map_size + (size_t)t * TW + (size_t)lane * 8;
-          *(uint64_t *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) = o;
-          if (o)
+          const size_t off = (size_t)k * a.map_size + (size_t)t * TW + (size_t)(lane & 31) * 8;
+          uint64_t m = 0;
+          if (lane < TW / 8) {
+            m = orb[b][k][lane] & *(const uint64_t *)(a.vcur + off);
+            orb[b][k][lane] = 0;
+          }
+          if (__ballot(m != 0)) {
+            tfl[k] |= 1ull << (t & 63);
+            if (lane < TW / 8) *(uint64_t *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) = m;
+          }
+          if (m)
             atomicOr((unsigned long long *)(a.segor + (size_t)seg * NC * a.map_size + off),
-                     (unsigned long long)o);
+                     (unsigned long long)m);
+          if ((t & 63) == 63 || t + 1 == ntiles) {
+            if (lane == 0) tfbase[k * a.nfw + (t >> 6)] = tfl[k];
+            tfl[k] = 0;
+          }
         }
       }
     };
@@ -793,24 +849,136 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
 }
 
 // DynamoRIO last-hash skip: skip[j] = hash[j] == hash[j-1] (hash[-1] = previous exec's).
-// A skipped trace must not touch the virgin map; pass 1 OR'ed it in, which is harmless only
-// when it equals its predecessor on the bytes has_new_bits looks at.  Otherwise its chunk is
-// queued (fix list) for recomputation without the skipped traces.
-__global__ void k_skip(const uint32_t *h32, const uint8_t *neq, uint32_t n,
-                       const uint32_t *prev_last /*[2] or null*/, const uint32_t *ctx_last,
-                       const uint32_t *global_last /*[2]*/, uint32_t *next_last,
-                       uint8_t *skip, uint32_t *flags, uint32_t *fix_list, uint32_t *fix_cnt) {
+// A skipped trace must not touch the virgin map.  Pass 1 OR'ed it into its chunk, which is
+// harmless when it equals its predecessor on the bytes has_new_bits examines (neq[j] == 0, exact
+// for every j > 0 of the shard: pass 1 compares row 0 of a chunk with the previous chunk's last
+// row) AND that predecessor's content is legitimately in the ORs or already in V.  So:
+//   bad[j]  = skip[j] && differs[j]   (a hash collision, or row 0 with an unknown / unclean
+//                                      predecessor)
+//   link[j] = skip[j] && !differs[j]  (same content as row j-1)
+// Every chunk holding a bad row, or a link row whose chain of links goes back to a bad row, is
+// recomputed without its skipped rows (fix list, k_total).
+//
+// k_skip (in kbz_shard_begin, rows j >= 1: they need no other shard) lists the chunks of bad
+// rows and queues those rows for k_chain.  It also publishes, in the shard's last-hash pair
+// (shard_last[1], bit 0 = non-empty), bit 1 = "has a bad row j >= 1" and bit 2 = "has a
+// non-skipped row j >= 1": a shard with bit 2 and without bit 1 ends in a clean row (its last
+// row's chain of links starts at a row that was applied), whatever its row 0 is.
+__global__ void k_skip(const uint32_t *h32, const uint8_t *neq, uint32_t n, uint8_t *skip,
+                       uint32_t *flags, uint32_t *fix_list, uint32_t *fix_cnt, uint32_t *bad_list,
+                       uint32_t *bad_cnt, uint32_t *shard_last) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j == 0) *next_last = global_last[1] ? global_last[0] : *ctx_last;
-  if (j >= n) return;
-  uint32_t hp;
-  if (j) hp = h32[j - 1];
-  else hp = prev_last ? prev_last[0] : *ctx_last;
-  const bool sk = h32[j] == hp;
-  skip[j] = sk;
-  if (sk && ((j % kChunk) == 0 || neq[j])) {
-    const uint32_t c = j / kChunk;
-    if (atomicExch(&flags[c], 1u) == 0u) fix_list[atomicAdd(fix_cnt, 1u)] = c;
+  bool applied = false, bad = false;
+  if (j >= 1 && j < n) {
+    const bool sk = h32[j] == h32[j - 1];
+    skip[j] = sk;
+    applied = !sk;
+    if (sk && neq[j]) {
+      bad = true;
+      const uint32_t c = j / kChunk;
+      if (atomicExch(&flags[c], 1u) == 0u) fix_list[atomicAdd(fix_cnt, 1u)] = c;
+      bad_list[atomicAdd(bad_cnt, 1u)] = j;
+    }
+  }
+  const uint64_t ap = __ballot(applied), bd = __ballot(bad);
+  if ((threadIdx.x & 63) == 0 && (ap || bd))
+    atomicOr(&shard_last[1], (bd ? 2u : 0u) | (ap ? 4u : 0u));
+}
+
+// Predecessor of the shard's row 0 (kbz_shard_link): unknown, the context's saved row (the
+// previous batch's last, clean iff *ok), or another shard's last row (clean iff its pair's
+// flags say so, see k_skip).
+enum { PRED_UNKNOWN = 0, PRED_SAVED = 1, PRED_PAIR = 2 };
+__device__ __forceinline__ bool pair_clean(uint32_t f) { return !(f & 2u) && (f & 4u); }
+
+struct ChainArgs {
+  uint32_t n;
+  const uint32_t *h32;
+  uint8_t *skip;
+  const uint8_t *neq;
+  const uint32_t *bad_list, *bad_cnt;
+  uint32_t *flags, *fix_list, *fix_cnt;
+  const uint32_t *prev_last;  // [2] predecessor hash (or null: ctx_last)
+  const uint32_t *ctx_last;
+  const uint32_t *global_last;  // [2]
+  uint32_t *next_last;
+  int pred_kind;
+  const uint32_t *pred_ok;   // PRED_SAVED: nonzero = clean; PRED_PAIR: the pair's flag word
+  const uint8_t *row0, *prow, *ignore;
+  uint32_t map_size;
+  const uint32_t *shard_flags;  // this shard's shard_last[1]
+  int single;                   // single-shard batch: the next saved row is our own last row
+  uint32_t *saved_ok;           // [1] clean flag of the next saved row (in/out)
+  const uint8_t *copy_src;      // row to save (or null), map_size bytes -> copy_dst
+  uint8_t *copy_dst;
+};
+
+// Row 0, then one wave per bad row (row 0 included when it is skipped and differs from its
+// predecessor, or the predecessor is unknown or unclean): follow its chain of link rows, 64 rows
+// per step, and list every chunk the chain enters (the bad row's own chunk is listed already).
+// Usually nothing is bad and block 0 returns after a few loads.  Blocks >= 1 copy the batch's
+// last row into the context (the next batch's row-0 predecessor).
+__global__ __launch_bounds__(256) void k_chain(ChainArgs a) {
+  if (blockIdx.x > 0) {
+    for (uint32_t i = ((blockIdx.x - 1) * blockDim.x + threadIdx.x) * 16; i < a.map_size;
+         i += (gridDim.x - 1) * blockDim.x * 16)
+      *(uint4 *)(a.copy_dst + i) = *(const uint4 *)(a.copy_src + i);
+    return;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t n = a.n;
+  bool bad0 = false;
+  if (n) {
+    const uint32_t hp = a.prev_last ? a.prev_last[0] : *a.ctx_last;
+    const bool sk0 = a.h32[0] == hp;
+    const bool known = a.pred_kind == PRED_SAVED ? *a.pred_ok != 0
+                       : a.pred_kind == PRED_PAIR ? pair_clean(*a.pred_ok) : false;
+    int diff = 0;
+    if (sk0 && known) {  // row 0 against its predecessor, 16 B per thread per step
+      for (uint32_t i = threadIdx.x * 16; i < a.map_size; i += blockDim.x * 16) {
+        const uint4 x = *(const uint4 *)(a.row0 + i), y = *(const uint4 *)(a.prow + i);
+        const uint64_t x0 = classify8((uint64_t)x.x | ((uint64_t)x.y << 32));
+        const uint64_t x1 = classify8((uint64_t)x.z | ((uint64_t)x.w << 32));
+        const uint64_t y0 = classify8((uint64_t)y.x | ((uint64_t)y.y << 32));
+        const uint64_t y1 = classify8((uint64_t)y.z | ((uint64_t)y.w << 32));
+        uint64_t r0 = ~0ull, r1 = ~0ull;
+        if (a.ignore) {
+          const uint4 g = *(const uint4 *)(a.ignore + i);
+          r0 = ~nonzero_bytes8((uint64_t)g.x | ((uint64_t)g.y << 32));
+          r1 = ~nonzero_bytes8((uint64_t)g.z | ((uint64_t)g.w << 32));
+        }
+        diff |= (((x0 ^ y0) & r0) | ((x1 ^ y1) & r1)) != 0;
+      }
+    }
+    diff = __syncthreads_or(diff);
+    bad0 = sk0 && (!known || diff);
+    if (threadIdx.x == 0) a.skip[0] = sk0;
+  }
+  __syncthreads();  // skip[0] is read by the chain walks below
+  if (threadIdx.x == 0) {
+    *a.next_last = a.global_last[1] ? a.global_last[0] : *a.ctx_last;
+    // clean flag of the row the context saves for the next batch
+    if (a.single) {
+      if (n) *a.saved_ok = (*a.bad_cnt == 0) && ((*a.shard_flags & 4u) || !bad0);
+    } else {
+      *a.saved_ok = a.copy_src ? pair_clean(a.global_last[1]) : 0u;
+    }
+  }
+  auto list = [&](uint32_t c) {
+    if (atomicExch(&a.flags[c], 1u) == 0u) a.fix_list[atomicAdd(a.fix_cnt, 1u)] = c;
+  };
+  const uint32_t cnt = *a.bad_cnt + (bad0 ? 1u : 0u);
+  for (uint32_t i = wave; i < cnt; i += blockDim.x / 64) {
+    const uint32_t b = (bad0 && i == cnt - 1) ? 0u : a.bad_list[i];
+    if (b == 0 && lane == 0) list(0);
+    for (uint32_t j0 = b + 1; j0 < n; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      const bool lk = j < n && a.skip[j] && !a.neq[j];
+      const uint64_t stop = __ballot(!lk);
+      const uint32_t len = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;  // links from j0 on
+      if (lane < len && (j % kChunk) == 0) list(j / kChunk);  // chunk starts on the chain
+      if (len < 64) break;
+    }
   }
 }
 
@@ -841,7 +1009,7 @@ __device__ __forceinline__ bool tile_stored(const uint64_t *tflags, uint32_t nfw
   return (tflags[((size_t)c * nclass + k) * nfw + (t >> 6)] >> (t & 63)) & 1;
 }
 __device__ void fix_column(const FixArgs &f, uint32_t map_size, uint32_t col, uint8_t *segor) {
-  const uint32_t cnt = *f.fix_cnt;
+  const uint32_t cnt = min(*f.fix_cnt, f.nchunks);
   for (uint32_t i = 0; i < cnt; i++) {
     const uint32_t chunk = f.fix_list[i];
     const uint64_t row0 = (uint64_t)chunk * kChunk;
@@ -1055,16 +1223,22 @@ __global__ __launch_bounds__(256) void k_resolve(const uint8_t *traces, size_t s
 }
 
 // Per-trace outputs, then re-arm the per-batch state for the next batch (no memsets between
-// batches): hnb32, the item and fix-list counters (the sticky error flags counters[1..2] stay
-// until kbz_sync reports them), the fix-list flags and the shard's last-hash pair.
+// batches): hnb32, the item, fix-list and bad-row counters and the row-0 flag (the sticky error
+// flags counters[1..2] stay until kbz_sync reports them), the fix-list flags and the shard's
+// last-hash pair.
 __global__ void k_pack(uint32_t *hnb32, const uint32_t *h32, uint32_t n, uint8_t *hnb_out,
                        uint32_t *h32_out, uint32_t *counters, uint32_t *flags, uint32_t nchunks,
                        uint32_t *shard_last) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j < nchunks && flags) flags[j] = 0;
   if (j == 0) {
+    counters[8] = counters[0];   // kbz_ctx_stats: claim items, recomputed chunks, bad rows
+    counters[9] = counters[3];
+    counters[10] = counters[4];
     counters[0] = 0;
     counters[3] = 0;
+    counters[4] = 0;
+    counters[5] = 0;
     shard_last[0] = 0;
     shard_last[1] = 0;
   }
@@ -1287,6 +1461,11 @@ struct kbz_ctx {
   uint32_t nfw = 1;
   uint32_t *flags = nullptr;     // [chunks] queued for recomputation
   uint32_t *fix_list = nullptr;  // [chunks]
+  uint32_t *bad_list = nullptr;  // [max_batch] DynamoRIO rows skipped but differing (k_skip)
+  uint8_t *saved_row = nullptr;  // [2][M] raw last row of the previous batch (row 0's
+  int srow = 0;                  // predecessor) is saved_row + srow*M; its clean flag counters[6+srow]
+  bool saved_valid = false;
+  int pass1 = KBZ_PASS1_AUTO;    // kbz_ctx_set_pass1
   uint8_t *skip = nullptr;
   uint8_t *neq = nullptr;
   uint32_t *h32 = nullptr;
@@ -1296,7 +1475,9 @@ struct kbz_ctx {
   uint8_t *total = nullptr;
   uint64_t *items = nullptr;
   uint32_t item_cap = 0;
-  uint32_t *counters = nullptr;  // [0] items, [1] overflow, [2] resolve error, [3] fix list
+  uint32_t *counters = nullptr;  // [0] items, [1] overflow, [2] resolve error, [3] fix list,
+                                 // [4] bad rows, [6..7] clean flags of the saved rows,
+                                 // [8..10] the last finished batch's [0], [3], [4]
   uint32_t *shard_last = nullptr;  // [2]
   // in-flight shard
   const uint8_t *cur_traces = nullptr;
@@ -1373,7 +1554,8 @@ int dalloc(T **p, size_t count) {
 void free_ctx(kbz_ctx *c) {
   if (!c) return;
   DevGuard g(c->device);
-  void *ptrs[] = {c->V[0], c->V[1], c->last, c->ignore, c->chunk_or, c->chunk_cls, c->tflags, c->flags, c->fix_list,
+  void *ptrs[] = {c->V[0], c->V[1], c->last, c->ignore, c->chunk_or, c->chunk_cls, c->tflags,
+                  c->flags, c->fix_list, c->bad_list, c->saved_row,
                   c->skip, c->neq, c->h32, c->hnb32, c->segor, c->segprev, c->total,
                   c->items, c->counters, c->shard_last, c->dslot[0], c->dslot[1],
                   c->dslot_oc[0], c->dslot_oc[1], c->dres_hnb, c->dres_h32, c->dres_x64};
@@ -1415,14 +1597,16 @@ constexpr uint32_t kWideBelowChunks = 512;  // 2 chunks per CU on a 256-CU MI355
 #ifndef KBZ_PASS1_DEPTH
 #define KBZ_PASS1_DEPTH 2
 #endif
-// Fewer chunks than two per CU (large maps, small batches): the wide-map variant.
-// KBZ_PASS1=narrow|wide overrides the choice (A/B timing).
-bool pass1_is_wide(uint32_t chunks) {
+// Fewer chunks than two per CU (large maps, small batches): the wide-map variant, unless the
+// context forces one (kbz_ctx_set_pass1; the environment KBZ_PASS1=narrow|wide sets a new
+// context's default, for A/B timing).
+bool pass1_is_wide(int choice, uint32_t chunks) {
 #ifdef KBZ_ABLATION
   return false;
 #else
-  static const char *force = getenv("KBZ_PASS1");
-  return force ? !strcmp(force, "wide") : chunks < kWideBelowChunks;
+  if (choice == KBZ_PASS1_NARROW) return false;
+  if (choice == KBZ_PASS1_WIDE) return true;
+  return chunks < kWideBelowChunks;
 #endif
 }
 #ifdef KBZ_ABLATION
@@ -1434,17 +1618,18 @@ void launch_abl(int depth, const Pass1Args &a, uint32_t chunks, hipStream_t s) {
 }
 #endif
 template <int MODE, bool IGN, bool X64>
-void launch_pass1(const Pass1Args &a, uint32_t chunks, hipStream_t s) {
+void launch_pass1(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s) {
 #ifdef KBZ_ABLATION
   // timing-only builds: KBZ_ABL selects the ablation, KBZ_DEPTH the register ring depth
   static const int abl = getenv("KBZ_ABL") ? atoi(getenv("KBZ_ABL")) : 0;
   static const int depth = getenv("KBZ_DEPTH") ? atoi(getenv("KBZ_DEPTH")) : KBZ_PASS1_DEPTH;
+  (void)choice;
   if (abl == 1) return launch_abl<MODE, IGN, X64, 1>(depth, a, chunks, s);
   if (abl == 2) return launch_abl<MODE, IGN, X64, 2>(depth, a, chunks, s);
   if (abl == 3) return launch_abl<MODE, IGN, X64, 3>(depth, a, chunks, s);
   return launch_abl<MODE, IGN, X64, 0>(depth, a, chunks, s);
 #else
-  if (pass1_is_wide(chunks))
+  if (pass1_is_wide(choice, chunks))
     hipLaunchKernelGGL((k_pass1w<MODE, IGN, X64, kWideNX, kWideNL, kWideD, kWideISO>),
                        dim3(chunks), dim3(64 * (kWideNL + kWideNX + kWideISO)), 0, s, a);
   else
@@ -1457,20 +1642,20 @@ int pass1_dispatch(kbz_ctx *c, const Pass1Args &a, uint32_t chunks, bool x64, hi
   const bool ign = c->ignore != nullptr && c->mode == KBZ_MODE_DYNAMORIO;
   switch (c->mode) {
     case KBZ_MODE_AFL:
-      x64 ? launch_pass1<KBZ_MODE_AFL, false, true>(a, chunks, s)
-          : launch_pass1<KBZ_MODE_AFL, false, false>(a, chunks, s);
+      x64 ? launch_pass1<KBZ_MODE_AFL, false, true>(c->pass1, a, chunks, s)
+          : launch_pass1<KBZ_MODE_AFL, false, false>(c->pass1, a, chunks, s);
       break;
     case KBZ_MODE_AFL_CLASSIFY:
-      x64 ? launch_pass1<KBZ_MODE_AFL_CLASSIFY, false, true>(a, chunks, s)
-          : launch_pass1<KBZ_MODE_AFL_CLASSIFY, false, false>(a, chunks, s);
+      x64 ? launch_pass1<KBZ_MODE_AFL_CLASSIFY, false, true>(c->pass1, a, chunks, s)
+          : launch_pass1<KBZ_MODE_AFL_CLASSIFY, false, false>(c->pass1, a, chunks, s);
       break;
     default:
       if (ign)
-        x64 ? launch_pass1<KBZ_MODE_DYNAMORIO, true, true>(a, chunks, s)
-            : launch_pass1<KBZ_MODE_DYNAMORIO, true, false>(a, chunks, s);
+        x64 ? launch_pass1<KBZ_MODE_DYNAMORIO, true, true>(c->pass1, a, chunks, s)
+            : launch_pass1<KBZ_MODE_DYNAMORIO, true, false>(c->pass1, a, chunks, s);
       else
-        x64 ? launch_pass1<KBZ_MODE_DYNAMORIO, false, true>(a, chunks, s)
-            : launch_pass1<KBZ_MODE_DYNAMORIO, false, false>(a, chunks, s);
+        x64 ? launch_pass1<KBZ_MODE_DYNAMORIO, false, true>(c->pass1, a, chunks, s)
+            : launch_pass1<KBZ_MODE_DYNAMORIO, false, false>(c->pass1, a, chunks, s);
   }
   HIP_TRY(hipGetLastError());
   return 0;
@@ -1511,17 +1696,21 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   c->max_batch = max_batch;
   c->max_chunks = cdiv(max_batch, kChunk);
   c->nfw = cdiv(map_size / kTileW, 64);
+  if (const char *force = getenv("KBZ_PASS1"))
+    c->pass1 = !strcmp(force, "wide") ? KBZ_PASS1_WIDE
+               : !strcmp(force, "narrow") ? KBZ_PASS1_NARROW : KBZ_PASS1_AUTO;
   const size_t M = map_size, nc = c->nc;
   c->item_cap = (uint32_t)std::min<size_t>(kItemsPerCol * M * nc + 1024, 0xffffffffu);
   bool ok = !dalloc(&c->V[0], 3 * M) && !dalloc(&c->V[1], 3 * M) && !dalloc(&c->last, 2) &&
             !dalloc(&c->chunk_or, c->max_chunks * nc * M) && !dalloc(&c->chunk_cls, c->max_chunks) &&
             !dalloc(&c->tflags, c->max_chunks * nc * c->nfw) &&
             !dalloc(&c->flags, c->max_chunks) && !dalloc(&c->fix_list, c->max_chunks) &&
+            !dalloc(&c->bad_list, max_batch) && !dalloc(&c->saved_row, 2 * M) &&
             !dalloc(&c->skip, max_batch) &&
             !dalloc(&c->neq, max_batch) && !dalloc(&c->h32, max_batch) &&
             !dalloc(&c->hnb32, max_batch) && !dalloc(&c->segor, kMaxSeg * nc * M) &&
             !dalloc(&c->segprev, kMaxSeg * nc * M) && !dalloc(&c->total, nc * M) &&
-            !dalloc(&c->items, c->item_cap) && !dalloc(&c->counters, 8) &&
+            !dalloc(&c->items, c->item_cap) && !dalloc(&c->counters, 16) &&
             !dalloc(&c->shard_last, 2);
   if (!ok) {
     std::string e = g_err;
@@ -1531,7 +1720,7 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   }
   (void)hipMemset(c->V[0], 0xff, 3 * M);
   (void)hipMemset(c->last, 0, 2 * sizeof(uint32_t));
-  (void)hipMemset(c->counters, 0, 8 * sizeof(uint32_t));
+  (void)hipMemset(c->counters, 0, 16 * sizeof(uint32_t));
   (void)hipMemset(c->shard_last, 0, 2 * sizeof(uint32_t));
   // consumers re-zero these for the next batch (k_total: segor, k_pack: hnb32)
   (void)hipMemset(c->segor, 0, kMaxSeg * nc * M);
@@ -1586,6 +1775,20 @@ int kbz_set_last_hash(kbz_ctx_t *c, uint32_t v) {
   DevGuard g(c->device);
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(c->last + c->lcur, &v, 4, hipMemcpyHostToDevice));
+  c->saved_valid = false;  // a restored hash comes without its trace: row 0 is checked blind
+  return 0;
+}
+int kbz_ctx_stats(kbz_ctx_t *c, uint32_t *out) {
+  if (!c || !out) return fail("null argument");
+  DevGuard g(c->device);
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, c->counters + 8, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+int kbz_ctx_set_pass1(kbz_ctx_t *c, int choice) {
+  if (!c) return fail("null ctx");
+  if (choice < KBZ_PASS1_AUTO || choice > KBZ_PASS1_WIDE) return fail("bad pass-1 choice");
+  c->pass1 = choice;
   return 0;
 }
 uint8_t *kbz_virgin_device(kbz_ctx_t *c) { return c ? c->V[c->vcur] : nullptr; }
@@ -1598,6 +1801,18 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
   if (n && check_rows(traces, stride, c->M)) return -1;
   DevGuard g(c->device);
   hipStream_t s = (hipStream_t)stream;
+  if (c->stage != 0) {
+    // the previous batch was abandoned between stages (e.g. a collective failed): re-arm what
+    // its later kernels would have reset -- the per-batch counters, fix-list flags, the shard's
+    // last-hash pair, the per-trace results and the segment aggregates
+    HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(uint32_t), s));  // [1..2] stay sticky
+    HIP_TRY(hipMemsetAsync(c->counters + 3, 0, 3 * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(c->flags, 0, c->max_chunks * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(c->shard_last, 0, 2 * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(c->hnb32, 0, c->max_batch * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(c->segor, 0, kMaxSeg * c->nc * c->M, s));
+    c->stage = 0;
+  }
   c->cur_traces = traces;
   c->cur_n = n;
   c->cur_stride = stride;
@@ -1634,6 +1849,12 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
   a.tflags = c->tflags;
   a.nfw = c->nfw;
   if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, s)) return -1;
+  if (c->mode == KBZ_MODE_DYNAMORIO) {  // the skip rule for rows j >= 1 needs no other shard
+    hipLaunchKernelGGL(k_skip, dim3(cdiv(n, 256)), dim3(256), 0, s, c->cur_h32, c->neq,
+                       (uint32_t)n, c->skip, c->flags, c->fix_list, c->counters + 3, c->bad_list,
+                       c->counters + 4, c->shard_last);
+    HIP_TRY(hipGetLastError());
+  }
   c->stage = 1;
   return 0;
 }
@@ -1647,19 +1868,71 @@ int kbz_shard_last_hash(kbz_ctx_t *c, uint32_t *d_out, void *stream) {
   return 0;
 }
 
-int kbz_shard_link(kbz_ctx_t *c, const uint32_t *prev_last, int is_first,
-                   const uint32_t *global_last, void *stream) {
+int kbz_shard_last_row(kbz_ctx_t *c, uint8_t *d_out, void *stream) {
+  if (!c || !d_out) return fail("null argument");
+  if (c->stage < 1) return fail("kbz_shard_last_row: call kbz_shard_begin first");
+  if (c->cur_n == 0) return 0;  // an empty shard has no last row (its pair says so)
+  DevGuard g(c->device);
+  HIP_TRY(hipMemcpyAsync(d_out, c->cur_traces + (c->cur_n - 1) * c->cur_stride, c->M,
+                         hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+
+int kbz_shard_link(kbz_ctx_t *c, const uint32_t *prev_last, const uint8_t *prev_row,
+                   int is_first, const uint32_t *global_last, const uint8_t *global_row,
+                   void *stream) {
   if (!c || c->stage != 1) return fail("kbz_shard_link: call kbz_shard_begin first");
   DevGuard g(c->device);
   hipStream_t s = (hipStream_t)stream;
   if (c->mode == KBZ_MODE_DYNAMORIO) {
-    const size_t n = c->cur_n;
+    const size_t n = c->cur_n, M = c->M;
     const int nl = c->lcur ^ 1;
-    hipLaunchKernelGGL(k_skip, dim3(std::max(1u, cdiv(n, 256))), dim3(256), 0, s, c->cur_h32,
-                       c->neq, (uint32_t)n, is_first ? nullptr : prev_last, c->last + c->lcur,
-                       global_last ? global_last : c->shard_last, c->last + nl, c->skip,
-                       c->flags, c->fix_list, c->counters + 3);
+    ChainArgs a{};
+    a.n = (uint32_t)n;
+    a.h32 = c->cur_h32;
+    a.skip = c->skip;
+    a.neq = c->neq;
+    a.bad_list = c->bad_list;
+    a.bad_cnt = c->counters + 4;
+    a.flags = c->flags;
+    a.fix_list = c->fix_list;
+    a.fix_cnt = c->counters + 3;
+    a.prev_last = is_first ? nullptr : prev_last;
+    a.ctx_last = c->last + c->lcur;
+    a.global_last = global_last ? global_last : c->shard_last;
+    a.next_last = c->last + nl;
+    // row 0's predecessor: the previous batch's last row (first shard) or the previous
+    // non-empty shard's last row; unknown or unclean -> row 0 counts as differing if skipped
+    if (is_first) {
+      a.pred_kind = c->saved_valid ? PRED_SAVED : PRED_UNKNOWN;
+      a.pred_ok = c->counters + 6 + c->srow;
+      a.prow = c->saved_row + c->srow * M;
+    } else {
+      a.pred_kind = (prev_row && prev_last) ? PRED_PAIR : PRED_UNKNOWN;
+      a.pred_ok = prev_last ? prev_last + 1 : nullptr;
+      a.prow = prev_row;
+    }
+    a.row0 = c->cur_traces;
+    a.ignore = c->ignore;
+    a.map_size = (uint32_t)M;
+    a.shard_flags = c->shard_last + 1;
+    // the batch's last row becomes the next batch's row-0 predecessor: the caller's global row
+    // (sharded), else this shard's own last row (a single-shard batch; an empty one keeps the
+    // old row).  It goes to the other saved slot: block 0 may still read the current one.
+    a.single = !global_row && !global_last;
+    a.copy_src = global_row ? global_row
+                 : (a.single && n) ? c->cur_traces + (n - 1) * c->cur_stride : nullptr;
+    a.copy_dst = c->saved_row + (c->srow ^ 1) * M;
+    a.saved_ok = c->counters + 6 + (c->srow ^ 1);
+    const unsigned copy_blocks = a.copy_src ? std::min(64u, cdiv(M / 16, 256)) : 0;
+    hipLaunchKernelGGL(k_chain, dim3(1 + copy_blocks), dim3(256), 0, s, a);
     HIP_TRY(hipGetLastError());
+    if (a.copy_src) {
+      c->srow ^= 1;
+      c->saved_valid = true;
+    } else if (!a.single) {
+      c->saved_valid = false;  // sharded without the last row: forget it
+    }
     c->lcur = nl;
     c->fix_pending = n != 0;  // k_total runs the (usually empty) fix path
   }
@@ -1739,7 +2012,7 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
     HIP_TRY(hipGetLastError());
   } else {
     // empty shard: k_skip may still have written the fix count / shard pair; re-arm them
-    HIP_TRY(hipMemsetAsync(c->counters + 3, 0, sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(c->counters + 3, 0, 3 * sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(c->shard_last, 0, 2 * sizeof(uint32_t), s));
   }
   c->vcur = vn;
@@ -1751,7 +2024,7 @@ int kbz_triage_batch_device(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_
                             const int8_t *outcome, uint8_t *hnb_out, uint32_t *h32_out,
                             uint64_t *x64_out, int want, void *stream) {
   if (kbz_shard_begin(c, traces, n, stride, outcome, h32_out, x64_out, want, stream)) return -1;
-  if (kbz_shard_link(c, nullptr, 1, nullptr, stream)) return -1;
+  if (kbz_shard_link(c, nullptr, nullptr, 1, nullptr, nullptr, stream)) return -1;
   if (kbz_shard_reduce(c, stream)) return -1;
   return kbz_shard_finish(c, nullptr, c->total, hnb_out, stream);
 }

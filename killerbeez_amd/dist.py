@@ -5,8 +5,10 @@ preserved, so the reference's sequential semantics hold across shards once every
 the OR of the coverage seen by the ranks before it:
 
   1. local pass over the shard (kbz_shard_begin: hashes, chunk aggregates)   -- no traffic
-  2. DynamoRIO only: all-gather of each shard's last hash32 (8 B per rank); the first trace
-     of a shard is compared with the last trace of the nearest non-empty earlier shard
+  2. DynamoRIO only: one all-gather of each shard's last hash32 and last raw trace (8 B +
+     map_size per rank); the first trace of a shard is compared with the last trace of the
+     nearest non-empty earlier shard (hash for the skip rule, row for its exactness), and every
+     rank remembers the batch's last row for the next batch
   3. local OR aggregate per virgin map (kbz_shard_reduce)
   4. all-gather of the aggregates (nclass * map_size bytes per rank) -> prefix = OR of earlier
      ranks, total = OR of all ranks.  RCCL has no bitwise reductions, so this is an
@@ -50,15 +52,20 @@ def triage_sharded(engine, traces, outcome, counts, rank, world, want=1, group=N
         timings.append(ev)
     nonempty = [r for r in range(world) if counts[r] > 0]
     if engine.mode == MODE_DYNAMORIO:
-        pair = torch.empty(2, dtype=torch.int32, device=device)
-        engine.shard_last_hash(pair)
-        pairs = _all_gather(pair, world, group) if world > 1 else pair.view(1, 2)
+        m = engine.map_size
+        buf = torch.zeros(m + 8, dtype=torch.uint8, device=device)  # [last row | hash pair]
+        engine.shard_last_row(buf[:m])
+        engine.shard_last_hash(buf[m:].view(torch.int32))
+        bufs = _all_gather(buf, world, group) if world > 1 else buf.view(1, -1)
+        rows, pairs = bufs[:, :m], bufs[:, m:].view(torch.int32)
         prev = [r for r in nonempty if r < rank]
-        prev_t = pairs[prev[-1]] if prev else None
-        glob_t = pairs[nonempty[-1]] if nonempty else None
-        engine.shard_link(prev_t, not prev, glob_t)
+        p = prev[-1] if prev else None
+        g = nonempty[-1] if nonempty else None
+        engine.shard_link(None if p is None else pairs[p], None if p is None else rows[p],
+                          not prev, None if g is None else pairs[g],
+                          None if g is None else rows[g])
     else:
-        engine.shard_link(None, True, None)
+        engine.shard_link(None, None, True, None, None)
     engine.shard_reduce()
     nb = engine.shard_aggregate_bytes()
     agg = torch.empty(nb, dtype=torch.uint8, device=device)

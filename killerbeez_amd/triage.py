@@ -17,6 +17,8 @@ MODE_AFL, MODE_DYNAMORIO, MODE_AFL_CLASSIFY = 0, 1, 2
 FUZZ_NONE, FUZZ_HANG, FUZZ_CRASH = 0, 1, 2
 WANT_H32, WANT_X64 = 1, 2
 MODES = {"afl": MODE_AFL, "dynamorio": MODE_DYNAMORIO, "afl_classify": MODE_AFL_CLASSIFY}
+PASS1_AUTO, PASS1_NARROW, PASS1_WIDE = 0, 1, 2
+PASS1 = {"auto": PASS1_AUTO, "narrow": PASS1_NARROW, "wide": PASS1_WIDE}
 
 
 def _np_ptr(a):
@@ -42,7 +44,7 @@ class TriageContext:
     (instrumentation/afl_instrumentation.h:12-34): virgin_bits/tmout/crash, last hash."""
 
     def __init__(self, map_size: int = 65536, mode: int | str = MODE_AFL,
-                 max_batch: int = 65536):
+                 max_batch: int = 65536, pass1: int | str | None = None):
         if isinstance(mode, str):
             mode = MODES[mode]
         self.map_size, self.mode, self.max_batch = int(map_size), int(mode), int(max_batch)
@@ -50,6 +52,20 @@ class TriageContext:
         self._h = L.kbz_ctx_create(self.map_size, self.mode, self.max_batch)
         if not self._h:
             raise KbzError("kbz_ctx_create: " + (L.kbz_last_error() or b"").decode())
+        if pass1 is not None:
+            self.set_pass1(pass1)
+
+    def set_pass1(self, choice: int | str) -> None:
+        """Force the pass-1 kernel ("auto" / "narrow" / "wide"; results are identical)."""
+        if isinstance(choice, str):
+            choice = PASS1[choice]
+        check(lib().kbz_ctx_set_pass1(self._h, int(choice)), "kbz_ctx_set_pass1")
+
+    def stats(self) -> dict:
+        """Work counters of the last finished batch (kbz_ctx_stats)."""
+        out = np.zeros(3, np.uint32)
+        check(lib().kbz_ctx_stats(self._h, _np_ptr(out)), "kbz_ctx_stats")
+        return {"claims": int(out[0]), "fixed_chunks": int(out[1]), "bad_rows": int(out[2])}
 
     # -- lifetime --------------------------------------------------------------------------
     def close(self):
@@ -207,11 +223,19 @@ class TriageContext:
                                         _stream_handle(stream)), "kbz_shard_last_hash")
         return out
 
-    def shard_link(self, prev_last, is_first, global_last, stream=None):
-        """prev_last / global_last: CUDA int32 tensors [2] (or None)."""
+    def shard_last_row(self, out, stream=None):
+        """Copy this shard's last raw trace into CUDA uint8 tensor out[map_size]."""
+        check(lib().kbz_shard_last_row(self._h, C.c_void_p(out.data_ptr()),
+                                       _stream_handle(stream)), "kbz_shard_last_row")
+        return out
+
+    def shard_link(self, prev_last, prev_row, is_first, global_last, global_row, stream=None):
+        """prev_last / global_last: CUDA int32 tensors [2] (or None); prev_row / global_row:
+        CUDA uint8 [map_size] last raw traces of those ranks (or None)."""
         ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())
-        check(lib().kbz_shard_link(self._h, ptr(prev_last), int(bool(is_first)), ptr(global_last),
-                                   _stream_handle(stream)), "kbz_shard_link")
+        check(lib().kbz_shard_link(self._h, ptr(prev_last), ptr(prev_row), int(bool(is_first)),
+                                   ptr(global_last), ptr(global_row), _stream_handle(stream)),
+              "kbz_shard_link")
 
     def shard_reduce(self, stream=None):
         check(lib().kbz_shard_reduce(self._h, _stream_handle(stream)), "kbz_shard_reduce")

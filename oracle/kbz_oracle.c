@@ -259,12 +259,15 @@ int kbzo_triage_batch(int mode, const uint8_t *traces, size_t n, size_t stride,
   return 0;
 }
 
-/* Multi-threaded exact variant (CPU baseline (ii)).  Decomposition:
- *   1. parallel: transform + hash every trace (hashes fix the DYNAMORIO skip set);
- *   2. parallel: per shard and per virgin map, OR of the (non-skipped) transformed traces;
- *   3. serial:   exclusive prefix of shard ORs -> each shard's entry virgin V & ~prefix;
- *   4. parallel: every shard replays the sequential rule from its entry virgin;
- *   5. V' = V & ~(OR of all shards).  Bytes hidden by ignore!=0 are never updated. */
+/* Multi-threaded exact variant (CPU baseline (ii)).  Decomposition, two reads
+ * of every trace:
+ *   A. parallel, per contiguous shard: transform + hash every trace (and XXH64), and OR the
+ *      transformed traces into the shard's per-map aggregate -- except the shard's first trace,
+ *      whose DYNAMORIO skip depends on the previous shard's last hash: it is kept aside;
+ *   B. serial:   skip of every shard's first trace, its row OR'ed in unless skipped; exclusive
+ *      prefix of the shard aggregates -> each shard's entry virgin V & ~prefix; V' = V & ~all;
+ *   C. parallel: every shard replays the sequential rule from its entry virgin (second read).
+ * Bytes hidden by ignore!=0 are never updated. */
 int kbzo_triage_batch_mt(int mode, const uint8_t *traces, size_t n, size_t stride,
                          size_t map_size, const int8_t *outcome, uint8_t *virgin,
                          const uint8_t *ignore, uint32_t *last_hash, int want,
@@ -274,34 +277,17 @@ int kbzo_triage_batch_mt(int mode, const uint8_t *traces, size_t n, size_t strid
   if (threads < 1) threads = 1;
   if ((size_t)threads > n) threads = n ? (int)n : 1;
   const size_t m = map_size, nmaps = (mode == KBZO_MODE_DYNAMORIO) ? 1 : 3;
+  const int dr = mode == KBZO_MODE_DYNAMORIO;
   uint32_t *h = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
   uint8_t *skip = (uint8_t *)calloc(n ? n : 1, 1);
   uint8_t *aggr = (uint8_t *)calloc((size_t)threads * nmaps * m, 1);
   uint8_t *entry = (uint8_t *)malloc((size_t)threads * nmaps * m);
-  if (!h || !skip || !aggr || !entry) {
-    free(h); free(skip); free(aggr); free(entry);
+  uint8_t *first = (uint8_t *)malloc((size_t)threads * m);
+  if (!h || !skip || !aggr || !entry || !first) {
+    free(h); free(skip); free(aggr); free(entry); free(first);
     return -1;
   }
   const uint32_t seed = 0xa5b35705u;
-#pragma omp parallel num_threads(threads)
-  {
-    uint8_t *t = (uint8_t *)malloc(m);
-#pragma omp for schedule(static)
-    for (size_t j = 0; j < n; j++) {
-      int oc = outcome ? outcome[j] : KBZO_FUZZ_NONE;
-      memcpy(t, traces + j * stride, m);
-      apply_xform(t, m, trace_xform(mode, oc));
-      h[j] = ignore ? kbzo_hash32_with_ignore(t, ignore, (uint32_t)m, seed)
-                    : kbzo_hash32(t, (uint32_t)m, seed);
-      if (x64_out && (want & KBZO_WANT_X64)) x64_out[j] = kbzo_xxh64(t, m, 0);
-    }
-    free(t);
-  }
-  uint32_t last = last_hash ? *last_hash : 0;
-  if (mode == KBZO_MODE_DYNAMORIO) {
-    for (size_t j = 0; j < n; j++) skip[j] = (h[j] == (j ? h[j - 1] : last));
-    if (n) last = h[n - 1];
-  }
 #pragma omp parallel num_threads(threads)
   {
 #ifdef _OPENMP
@@ -312,15 +298,32 @@ int kbzo_triage_batch_mt(int mode, const uint8_t *traces, size_t n, size_t strid
     size_t lo = n * (size_t)s / threads, hi = n * (size_t)(s + 1) / threads;
     uint8_t *t = (uint8_t *)malloc(m);
     for (size_t j = lo; j < hi; j++) {
-      if (skip[j]) continue;
       int oc = outcome ? outcome[j] : KBZO_FUZZ_NONE;
-      memcpy(t, traces + j * stride, m);
-      apply_xform(t, m, trace_xform(mode, oc));
+      uint8_t *x = (j == lo) ? first + (size_t)s * m : t;
+      memcpy(x, traces + j * stride, m);
+      apply_xform(x, m, trace_xform(mode, oc));
+      h[j] = ignore ? kbzo_hash32_with_ignore(x, ignore, (uint32_t)m, seed)
+                    : kbzo_hash32(x, (uint32_t)m, seed);
+      if (x64_out && (want & KBZO_WANT_X64)) x64_out[j] = kbzo_xxh64(x, m, 0);
+      if (j == lo) continue;
+      if (dr && (skip[j] = h[j] == h[j - 1])) continue;
       uint8_t *a = aggr + ((size_t)s * nmaps + trace_map(mode, oc)) * m;
-      for (size_t i = 0; i < m; i++) a[i] |= t[i];
+      for (size_t i = 0; i < m; i++) a[i] |= x[i];
     }
     free(t);
   }
+  uint32_t last = last_hash ? *last_hash : 0;
+  for (int s = 0; s < threads; s++) {
+    const size_t lo = n * (size_t)s / threads, hi = n * (size_t)(s + 1) / threads;
+    if (lo == hi) continue;
+    if (dr) skip[lo] = h[lo] == (lo ? h[lo - 1] : last);
+    if (skip[lo]) continue;
+    int oc = outcome ? outcome[lo] : KBZO_FUZZ_NONE;
+    uint8_t *a = aggr + ((size_t)s * nmaps + trace_map(mode, oc)) * m;
+    const uint8_t *x = first + (size_t)s * m;
+    for (size_t i = 0; i < m; i++) a[i] |= x[i];
+  }
+  if (dr && n) last = h[n - 1];
   for (size_t k = 0; k < nmaps; k++) {
     uint8_t *v = virgin + k * m;
     for (size_t i = 0; i < m; i++) {
@@ -356,7 +359,7 @@ int kbzo_triage_batch_mt(int mode, const uint8_t *traces, size_t n, size_t strid
     free(t);
   }
   if (last_hash) *last_hash = last;
-  free(h); free(skip); free(aggr); free(entry);
+  free(h); free(skip); free(aggr); free(entry); free(first);
   return 0;
 }
 

@@ -43,6 +43,29 @@ uint8_t REF_NAME(ref_afl_has_new_bits)(uint8_t *virgin, uint8_t *trace) {
 void REF_NAME(ref_afl_simplify_trace)(uint8_t *trace) { simplify_trace((uint64_t *)trace); }
 void REF_NAME(ref_afl_merge_bitmaps)(uint8_t *dest, const uint8_t *src) { merge_bitmaps(dest, src); }
 size_t REF_NAME(ref_afl_map_size)(void) { return MAP_SIZE; }
+/* The merger's fold (merger/merger.c:79-99 -> afl_merge afl_instrumentation.c:123-140) over n
+ * in-memory states, each virgin_bits|virgin_tmout|virgin_crash (3*MAP_SIZE bytes), with the
+ * reference's own merge_bitmaps; the JSON decode and per-state malloc of the CLI are left out
+ * (their encoding lives in the absent killerbeez-utils).  acc: 3*MAP_SIZE, in/out.  The CPU
+ * baseline of bench.py --workload merge ("kind": "reference"). */
+void REF_NAME(ref_afl_merge_loop)(uint8_t *acc, const uint8_t *states, size_t n) {
+  for (size_t s = 0; s < n; s++)
+    for (int k = 0; k < 3; k++)
+      merge_bitmaps(acc + (size_t)k * MAP_SIZE, states + (s * 3 + k) * (size_t)MAP_SIZE);
+}
+/* finish_fuzz_round's novelty step (afl_instrumentation.c:231-274) exec after exec: EXIT -> raw
+ * trace vs virgin_bits; HANG / CRASH (outcome 1 / 2) -> simplify_trace, then virgin_tmout /
+ * virgin_crash.  virgin: the 3 maps; scratch: MAP_SIZE bytes (the SHM trace_bits copy). */
+void REF_NAME(ref_afl_triage_loop)(const uint8_t *traces, size_t n, size_t stride,
+                                   const int8_t *outcome, uint8_t *virgin, uint8_t *hnb_out,
+                                   uint8_t *scratch) {
+  for (size_t j = 0; j < n; j++) {
+    const int oc = outcome ? outcome[j] : 0;
+    memcpy(scratch, traces + j * stride, MAP_SIZE);
+    if (oc == 1 || oc == 2) simplify_trace((uint64_t *)scratch);
+    hnb_out[j] = has_new_bits(virgin + (size_t)oc * MAP_SIZE, scratch);
+  }
+}
 
 #elif defined(REF_DR)
 #include "winafl_types.h" /* /root/reference/instrumentation/winafl_types.h */

@@ -24,13 +24,10 @@ def test_hip_library_exports_header():
     missing = [f for f in declared if f not in exported]
     assert not missing, missing
     assert {n for n, _, _ in _lib.SIGNATURES} == set(declared)
-    assert L.kbz_abi_version() == 1
+    assert L.kbz_abi_version() == _lib.ABI_VERSION
 
 
 def test_hip_library_is_gfx950():
-    out = subprocess.check_output(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--list",
-                                   "--type=o", f"--input={kbuild.HIP_LIB}"], text=True,
-                                  stderr=subprocess.STDOUT) if False else ""
     # the fat binary embeds a gfx950 code object
     data = open(kbuild.HIP_LIB, "rb").read()
     assert b"gfx950" in data

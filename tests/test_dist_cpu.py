@@ -49,6 +49,7 @@ class CpuShardEngine:
     def __init__(self, mode, virgin, last_hash=0):
         self.mode = mode
         self.nc = 1 if mode == oracle.MODE_DYNAMORIO else 3
+        self.map_size = M
         self.V = virgin.copy()
         self.last = last_hash
 
@@ -59,13 +60,21 @@ class CpuShardEngine:
         self.h = np.array([oracle.hash32(r) for r in self.x], np.uint32)
         return {}
 
+    def shard_last_row(self, out):
+        if self.t.shape[0]:
+            out.copy_(torch.from_numpy(self.t[-1]))
+
     def shard_last_hash(self, out):
         n = self.t.shape[0]
         out[0] = int(np.int32(np.uint32(self.h[-1] if n else 0).view(np.int32)))
         out[1] = 1 if n else 0
 
-    def shard_link(self, prev_t, is_first, glob_t):
+    def shard_link(self, prev_t, prev_row, is_first, glob_t, glob_row):
         n = self.t.shape[0]
+        if not is_first:  # the previous shard's last row travels with its hash
+            assert prev_row is not None and int(prev_t[1]) == 1
+            assert oracle.hash32(_xform(self.mode, prev_row.numpy()[None], [0])[0]) == \
+                np.uint32(np.int32(prev_t[0].item()))
         self.prev = self.last if is_first else int(np.uint32(np.int32(prev_t[0].item())))
         self.skip = np.zeros(n, bool)
         if self.mode == oracle.MODE_DYNAMORIO:

@@ -103,8 +103,9 @@ def test_merge_oracle(oracle_lib):
 # ---- the gfx950 path on the same vectors -----------------------------------------------------
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pass1", ["narrow", "wide"])
 @pytest.mark.parametrize("name,mode", MODES)
-def test_triage_gpu(gpu, name, mode):
+def test_triage_gpu(gpu, name, mode, pass1):
     import torch
 
     from killerbeez_amd.triage import WANT_H32, WANT_X64, TriageContext
@@ -112,7 +113,7 @@ def test_triage_gpu(gpu, name, mode):
     f = load("triage.npz")
     m = int(f["map_size"])
     t = dense(int(f["n"]), m, f["tj"], f["ti"], f["tv"])
-    with TriageContext(m, mode, t.shape[0]) as ctx:
+    with TriageContext(m, mode, t.shape[0], pass1=pass1) as ctx:
         out = ctx.triage(torch.from_numpy(t).cuda(), torch.from_numpy(f["outcome"]).cuda(),
                          WANT_H32 | WANT_X64)
         torch.cuda.synchronize()
@@ -127,7 +128,8 @@ def test_triage_gpu(gpu, name, mode):
 
 
 @pytest.mark.gpu
-def test_triage_ignore_gpu(gpu):
+@pytest.mark.parametrize("pass1", ["narrow", "wide"])
+def test_triage_ignore_gpu(gpu, pass1):
     import torch
 
     from killerbeez_amd.triage import WANT_H32, TriageContext
@@ -135,7 +137,7 @@ def test_triage_ignore_gpu(gpu):
     f = load("triage.npz")
     m = int(f["map_size"])
     t = dense(int(f["ign_n"]), m, f["ign_tj"], f["ign_ti"], f["ign_tv"])
-    with TriageContext(m, oracle.MODE_DYNAMORIO, t.shape[0]) as ctx:
+    with TriageContext(m, oracle.MODE_DYNAMORIO, t.shape[0], pass1=pass1) as ctx:
         ctx.set_ignore(f["ign_bytes"])
         out = ctx.triage(torch.from_numpy(t).cuda(), None, WANT_H32)
         torch.cuda.synchronize()

@@ -18,6 +18,15 @@ pytestmark = pytest.mark.gpu
 MODES = [MODE_AFL, MODE_DYNAMORIO, MODE_AFL_CLASSIFY]
 
 
+@pytest.fixture(autouse=True, params=["narrow", "wide"])
+def pass1(request, monkeypatch):
+    """Every case runs through both pass-1 kernels: k_pass1s (narrow; what AUTO picks for
+    batches of >= 512 chunks, e.g. config 2) and k_pass1w (wide; AUTO's pick below that).
+    kbz_ctx_create reads KBZ_PASS1 as the new context's default."""
+    monkeypatch.setenv("KBZ_PASS1", request.param)
+    return request.param
+
+
 def gpu_triage(ctx, traces, oc, want=WANT_H32 | WANT_X64):
     import torch
 
@@ -277,15 +286,21 @@ def _run_shards(ctxs, shards, ocs, mode, device):
     outs = [c.shard_begin(s, o, WANT_H32) for c, s, o in zip(ctxs, shards, ocs)]
     nonempty = [r for r in range(world) if counts[r] > 0]
     if mode == MODE_DYNAMORIO:
+        m = ctxs[0].map_size
         pairs = torch.stack([c.shard_last_hash(torch.empty(2, dtype=torch.int32, device=device))
                              for c in ctxs])
+        rows = torch.stack([c.shard_last_row(torch.zeros(m, dtype=torch.uint8, device=device))
+                            for c in ctxs])
         for r, c in enumerate(ctxs):
             prev = [q for q in nonempty if q < r]
-            c.shard_link(pairs[prev[-1]] if prev else None, not prev,
-                         pairs[nonempty[-1]] if nonempty else None)
+            p = prev[-1] if prev else None
+            g = nonempty[-1] if nonempty else None
+            c.shard_link(None if p is None else pairs[p], None if p is None else rows[p],
+                         not prev, None if g is None else pairs[g],
+                         None if g is None else rows[g])
     else:
         for c in ctxs:
-            c.shard_link(None, True, None)
+            c.shard_link(None, None, True, None, None)
     for c in ctxs:
         c.shard_reduce()
     nb = ctxs[0].shard_aggregate_bytes()
@@ -445,3 +460,201 @@ def test_triage_modules_per_module_coverage(gpu):
         np.testing.assert_array_equal(anyv.cpu().numpy(), exp_any)
     for c in ctxs:
         c.close()
+
+
+# ---- at scale: >= 512 chunks, so AUTO picks k_pass1s (the config-2 kernel) ------------------
+N_AT_SCALE = 32768 + 37  # 513 chunks, the last one partial
+
+
+@pytest.mark.parametrize("mode", [MODE_AFL, MODE_AFL_CLASSIFY])
+@pytest.mark.parametrize("m", [256, 4096])
+def test_at_scale_afl_outcome_routing(gpu, mode, m):
+    """3 virgin maps (finish_fuzz_round afl_instrumentation.c:231-274): 5 % hangs + crashes go
+    simplified to virgin_tmout / virgin_crash, with all-zero traces (simplify's 0x01 words) and
+    identical neighbours; XXH64 on; a second batch carries the three maps."""
+    t, oc = synth.sparse_np(N_AT_SCALE, m, seed=231 + m + mode, hot_frac=0.05,
+                            outcome_p=(0.95, 0.02, 0.03))
+    t[100:110] = 0
+    t[640:700] = t[639]
+    oc[640:700] = oracle.FUZZ_CRASH
+    ctx = TriageContext(m, mode, N_AT_SCALE)
+    e1 = check(mode, t, oc, ctx=ctx)
+    for k in range(3):
+        assert (e1["hnb"][oc == k] > 0).any()
+    t2, oc2 = synth.sparse_np(N_AT_SCALE, m, seed=232 + m + mode, hot_frac=0.05,
+                              outcome_p=(0.9, 0.05, 0.05))
+    check(mode, t2, oc2, ctx=ctx)
+    ctx.close()
+
+
+def _collide(t, j, zc, rng, k=12):
+    """Row j = row j-1 except on k bytes that the ignore map hides from hash32_with_ignore but
+    has_new_bits_with_ignore examines: equal hashes, different content (a collision)."""
+    t[j] = t[j - 1]
+    t[j, rng.choice(zc, k)] = rng.integers(1, 256, k)
+
+
+def _expected_fix(t, h32, ign, last_hash, prev_row, prev_clean=True):
+    """What the skip fix path must recompute (kbz_triage.hip k_skip / k_chain), from first
+    principles: skip[j] = h[j] == h[j-1]; a skipped row that differs from its predecessor on
+    the examined bytes -- or, for row 0, whose predecessor (the previous batch's last row) is
+    unknown or not clean -- is bad; every chunk holding a bad row or a repeat chained to one is
+    recomputed.  The batch's last row is then clean (never excluded from V while its repeats
+    were applied) by the engine's conservative rule: no bad row j >= 1, and some row j >= 1
+    applied or row 0 not bad.  Returns (bad rows j >= 1, recomputed chunks, last row clean)."""
+    lut = oracle.count_class_table()
+    x = lut[t]
+    rel = np.ones(t.shape[1], bool) if ign is None else ign == 0
+    n = t.shape[0]
+    prevh = np.concatenate([[last_hash], h32[:-1]]).astype(np.uint32)
+    skip = h32 == prevh
+    differs = np.zeros(n, bool)
+    differs[1:] = ((x[1:] != x[:-1]) & rel).any(axis=1)
+    differs[0] = (prev_row is None or not prev_clean or
+                  ((x[0] != lut[prev_row]) & rel).any())
+    bad = skip & differs
+    chunks = set()
+    for r in np.nonzero(bad)[0]:
+        chunks.add(r // 64)
+        j = r + 1
+        while j < n and skip[j] and not differs[j]:
+            if j % 64 == 0:
+                chunks.add(j // 64)
+            j += 1
+    clean = not bad[1:].any() and ((~skip[1:]).any() or not bad[0])
+    return int(bad[1:].sum()), chunks, clean
+
+
+def test_at_scale_dynamorio_repeats_and_collisions(gpu, pass1):
+    """has_new_coverage (dynamorio_instrumentation.c:1428-1468) at 513 chunks with ignore bytes:
+    exact repeats everywhere, at chunk starts (lane 0, compared with the previous chunk's last
+    row), runs over several chunks; collisions inside chunks and at lane 0, one followed by a
+    700-row chain of repeats (every chunk the chain enters must be recomputed).  Then batches
+    whose row 0 repeats the previous batch's last exec: when that exec was a collision (never
+    applied: its repeats must not be applied either), when it was clean (nothing to recompute),
+    and when row 0 collides with it (row 0 and its chain are recomputed)."""
+    m = 4096
+    rng = np.random.default_rng(1428)
+    t, oc = synth.sparse_np(N_AT_SCALE, m, seed=1429, hot_frac=0.05)
+    ign = np.where(rng.random(m) < 0.4, 0, rng.integers(1, 256, size=m)).astype(np.uint8)
+    zc = np.nonzero(ign == 0)[0]
+    for c in range(1, 513, 3):
+        t[64 * c] = t[64 * c - 1]           # exact repeat at lane 0
+    for j in rng.integers(1, N_AT_SCALE, 400):
+        t[j] = t[j - 1]                     # exact repeats anywhere
+    t[5000:5300] = t[4999]                  # a run over several chunks
+    for j in [64 * 7, 64 * 11, 777, 5555, 20001, N_AT_SCALE - 1]:
+        _collide(t, j, zc, rng)
+    _collide(t, 9000, zc, rng)              # a collision, then a chain of repeats of it
+    t[9001:9700] = t[9000]
+    ctx = TriageContext(m, MODE_DYNAMORIO, N_AT_SCALE)
+    ctx.set_ignore(ign)
+    exp = check(MODE_DYNAMORIO, t, oc, ignore=ign, ctx=ctx)
+    nbad, chunks, clean = _expected_fix(t, exp["h32"], ign, 0, None)
+    assert nbad >= 7 and set(range(141, 152)) <= chunks and len(chunks) < 40 and not clean
+    st = ctx.stats()
+    assert (st["fixed_chunks"], st["bad_rows"]) == (len(chunks), nbad)
+    last, prev = exp["last_hash"], t[-1].copy()
+    batches = []
+    t2, oc2 = synth.sparse_np(4000, m, seed=1430, hot_frac=0.05)
+    t2[0] = t[-1]                           # repeats the last exec, a collision (not clean)
+    t2[1:300] = t2[0]
+    batches.append((t2, {0, 1, 2, 3, 4}))
+    t3 = t2.copy()
+    t3[0] = t2[-1]
+    t3[0, rng.choice(zc, 12)] = rng.integers(1, 256, 12)  # collides with the (clean) last exec
+    t3[1:200] = t3[0]
+    batches.append((t3, {0, 1, 2, 3}))
+    t4 = synth.sparse_np(4000, m, seed=1431, hot_frac=0.05)[0]
+    t4[0] = t3[-1]                          # repeats the (clean) last exec: nothing to redo
+    t4[1:100] = t4[0]
+    batches.append((t4, set()))
+    for tb, want_chunks in batches:
+        e = check(MODE_DYNAMORIO, tb, oc2, ignore=ign, ctx=ctx)
+        assert e["hnb"][0] == 0
+        nb, ch, cl = _expected_fix(tb, e["h32"], ign, last, prev, clean)
+        assert ch == want_chunks and nb == 0
+        st = ctx.stats()
+        assert (st["fixed_chunks"], st["bad_rows"]) == (len(ch), nb)
+        last, prev, clean = e["last_hash"], tb[-1].copy(), cl
+    ctx.close()
+
+
+def test_dynamorio_restored_hash_unknown_predecessor(gpu):
+    """kbz_set_last_hash (state restore) forgets the previous trace: a repeated first exec is
+    then handled without it -- row 0 and its chain of repeats (3 chunks) are recomputed."""
+    m = 4096
+    t, oc = synth.sparse_np(40000, m, seed=1461, hot_frac=0.05)
+    t[1:150] = t[0]
+    exp_h0 = oracle.triage_batch(MODE_DYNAMORIO, t[:1], None)["h32"][0]
+    ctx = TriageContext(m, MODE_DYNAMORIO, 40000)
+    ctx.last_hash = int(exp_h0)
+    exp = check(MODE_DYNAMORIO, t, oc, ctx=ctx)
+    assert exp["hnb"][0] == 0
+    assert ctx.stats()["fixed_chunks"] == 3
+    ctx.close()
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_at_scale_x64_partial_chunk(gpu, mode):
+    m = 256
+    t, oc = synth.sparse_np(N_AT_SCALE, m, seed=855 + mode, hot_frac=0.1)
+    check(mode, t, oc, want=WANT_H32 | WANT_X64)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_abandoned_batch_is_rearmed(gpu, mode):
+    """A batch abandoned between the sharded stages (e.g. a failed collective) leaves per-batch
+    state behind; the next kbz_shard_begin re-arms it and the next batch is exact."""
+    import torch
+
+    m = 4096
+    t, oc = synth.sparse_np(3000, m, seed=1593, hot_frac=0.05)
+    t[64] = t[63]
+    ctx = TriageContext(m, mode, 3000)
+    v0, l0 = ctx.get_virgin(), ctx.last_hash
+    tt, oo = torch.from_numpy(t).cuda(), torch.from_numpy(oc).cuda()
+    ctx.shard_begin(tt, oo, WANT_H32)
+    ctx.shard_link(None, None, True, None, None)
+    ctx.shard_reduce()
+    torch.cuda.synchronize()                # abandoned here: no shard_finish
+    ctx.set_virgin(v0)
+    ctx.last_hash = l0
+    small = t[:500]
+    check(mode, small, oc[:500], ctx=ctx)
+    ctx.close()
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_config3_dense_1m(gpu, mode):
+    """BASELINE config 3's traces (dense: 50 % hot, counts U[1,255]) at 1 MiB, at a batch size
+    the sequential oracle checks in seconds, crash/hang mixed in."""
+    t, oc = synth.dense_np(300, 1 << 20, seed=3 + mode, outcome_p=(0.8, 0.1, 0.1))
+    t[65] = t[64]
+    check(mode, t, oc)
+
+
+@pytest.mark.slow
+def test_full_size_config3(gpu):
+    """BASELINE config 3 at full size: 16,384 dense traces x 1 MiB (16 GiB), DynamoRIO mode,
+    exactly against the sharded CPU oracle, then idempotence."""
+    import torch
+
+    n, m = 16384, 1 << 20
+    t, oc = synth.dense_torch(n, m, seed=0x5EED, device="cuda")
+    ctx = TriageContext(m, MODE_DYNAMORIO, n)
+    out = ctx.triage(t, oc, WANT_H32)
+    torch.cuda.synchronize()
+    ctx.sync()
+    th = t.cpu().numpy()
+    exp = oracle.triage_batch(MODE_DYNAMORIO, th, oc.cpu().numpy(), threads=16)
+    del th
+    np.testing.assert_array_equal(out["hnb"].cpu().numpy(), exp["hnb"])
+    np.testing.assert_array_equal(out["h32"].cpu().numpy().view(np.uint32), exp["h32"])
+    v = ctx.get_virgin()
+    np.testing.assert_array_equal(v, exp["virgin"])
+    out2 = ctx.triage(t, oc, WANT_H32)
+    torch.cuda.synchronize()
+    assert int(out2["hnb"].max()) == 0
+    np.testing.assert_array_equal(ctx.get_virgin(), v)
+    ctx.close()
