@@ -1,26 +1,40 @@
 #!/usr/bin/env python3
 """Headline benchmark: traces triaged/s (64 KiB map, classify + novelty + hash32) on MI355X.
 
-Workload (BASELINE.json configs[1]): per GPU a batch of 65,536
+Workload (BASELINE.json configs[1]): per GPU, batches of 65,536
 synthetic sparse traces x 64 KiB raw hit counters (seeded generator in killerbeez_amd.synth,
-generated directly in HBM), triaged with DynamoRIO semantics (dynamorio_instrumentation.c:
+generated directly in HBM; every batch is a different sample of the same target program: they
+share the hot edge set), triaged with DynamoRIO semantics (dynamorio_instrumentation.c:
 1428-1468: classify_counts, hash32, last-hash skip, has_new_bits vs virgin_bits).  One step =
-one full triage of one batch; the virgin map and last hash carry over from step to step
-(steady-state fuzzing), cycling through a pool of distinct batches.
+one full triage of one batch; the virgin map and last hash carry over from step to step.
 
-With --gpus N (launched by torch.distributed.run) every rank triages its own 65,536-trace
-shard of an N x 65,536-trace global batch with the exact sharded protocol of
-killerbeez_amd.dist (RCCL all-gathers) -- weak scaling.
+`value` is measured on FRESH batches: every warmup and timed step triages a batch it has never
+seen (pool = warmup + steps distinct batches, 4 GiB each), so the novelty scan and claim
+resolution do real work.  Also reported ("variants"): the same steps on already-absorbed
+batches (steady state: nothing new), fresh batches in which 90 % of execs repeat their
+predecessor (the last-hash skip path), and the first batch on all-0xff virgin maps.
+
+With --gpus N every rank triages its own 65,536-trace shard of an N x 65,536-trace global
+batch with the exact sharded protocol of killerbeez_amd.dist (RCCL all-gathers) -- weak
+scaling.  Without an outside launcher, `--gpus N` (N > 1) starts N ranks itself
+(torch.distributed.run, 127.0.0.1) from a parent that never touches the GPU.
 
 Prints ONE JSON line (rank 0).  Also reports the dominant kernel's (pass 1) achieved
-algorithmic HBM bandwidth against the 8 TB/s peak, and the reference CPU path timed on this
-host's cores on a bounded sample.
+algorithmic HBM bandwidth against the 8 TB/s peak (HIP events around each pass-1 launch), and
+the reference CPU path timed on this host's cores on a bounded sample.
+
+Other workloads: --workload config3 (16,384 dense x 1 MiB), merge (config 4: 100k merger
+states AND-folded, sharded over the ranks), stream (config 5: traces from host memory through
+the pinned ingest ring + the unique crash/hang table, PCIe-bound), plugin (per-exec latency of
+the instrumentation plugin at batch sizes 1/16/256/4096).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -39,16 +53,18 @@ def parse():
     p.add_argument("--batch", type=int, default=65536, help="traces per GPU per step")
     p.add_argument("--map-size", type=int, default=65536)
     p.add_argument("--mode", default="dynamorio", choices=["dynamorio", "afl", "afl_classify"])
-    p.add_argument("--pool", type=int, default=2, help="distinct batches cycled through")
+    p.add_argument("--pool", type=int, default=0,
+                   help="distinct batches (default warmup + steps, capped by free HBM)")
+    p.add_argument("--repeat-frac", type=float, default=0.9)
+    p.add_argument("--no-variants", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--pmc", action="store_true",
+                   help="measure roofline.traffic live: two rocprofv3 --pmc passes of a child run")
     p.add_argument("--seed", type=int, default=0x5EED)
     p.add_argument("--workload", default="config2",
-                   choices=["config2", "config3", "merge", "stream"],
-                   help="config2 (default, the headline): 65,536 sparse x 64 KiB; config3: "
-                        "16,384 dense x 1 MiB; merge: 100k merger states AND-folded; stream: "
-                        "config2 traces from host memory through the pinned ring (PCIe-bound)")
-    p.add_argument("--states", type=int, default=100000, help="merge workload: states")
+                   choices=["config2", "config3", "merge", "stream", "plugin"])
+    p.add_argument("--states", type=int, default=100000, help="merge workload: states (total)")
     a = p.parse_args()
     if a.workload == "config3":
         if a.batch == 65536:
@@ -58,10 +74,88 @@ def parse():
     return a
 
 
-def cpu_baseline(traces_dev, mode, seconds):
-    """Reference CPU path (oracle/_ref: the reference's own classify_counts + hash32 +
-    has_new_bits in has_new_coverage's control flow), one core, on a bounded sample of the
-    same workload.  Falls back to the clean-room restatement if _ref is absent."""
+# ---- launching ---------------------------------------------------------------------------------
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def maybe_launch(args):
+    """--gpus N > 1 without an outside torch.distributed.run: start the N ranks as children
+    (this process has not touched the GPU) and exit with their status."""
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+               "--master-port", str(_free_port()), os.path.abspath(__file__), *sys.argv[1:]]
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        sys.exit(subprocess.call(cmd, env=env))
+
+
+def init_dist():
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    return world, rank, dev
+
+
+def barrier_sync(world, dev):
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier(device_ids=[dev.index])
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world, dev):
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def finish(world):
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ---- CPU baselines -----------------------------------------------------------------------------
+
+def usable_cores():
+    """Cores this process may run on: its affinity mask, capped by a cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(float(quota) // float(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_baseline(traces_dev, outcome_dev, mode, seconds):
+    """The reference's own per-exec novelty step (oracle/_ref: classify_counts + hash32 +
+    has_new_bits in has_new_coverage's control flow for DynamoRIO; finish_fuzz_round's
+    simplify + has_new_bits routing for AFL), one core, on a bounded sample of the same
+    workload.  Falls back to the clean-room restatement if _ref is absent."""
     import ctypes as C
 
     import numpy as np
@@ -69,150 +163,217 @@ def cpu_baseline(traces_dev, mode, seconds):
     import oracle
 
     m = traces_dev.shape[1]
-    sample_n = min(traces_dev.shape[0], 8192)
+    sample_n = min(traces_dev.shape[0], 8192 if m <= 65536 else 512)
     host = traces_dev[:sample_n].cpu().numpy()
-    virgin = np.full(m, 0xFF, np.uint8)
+    oc = outcome_dev[:sample_n].cpu().numpy().astype(np.int8)
+    virgin = np.full(3 * m, 0xFF, np.uint8)
     scratch = np.empty(m, np.uint8)
     hnb = np.zeros(sample_n, np.uint8)
     last = C.c_uint32(0)
     sfx = {65536: "64k", 1 << 20: "1m"}.get(m)
-    kind = "reference"
-    fn = None
-    if mode == 1 and sfx and oracle.have_ref():
-        fn = getattr(oracle.ref(), f"ref_dr_triage_loop_{sfx}")
-        fn.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p,
-                       C.c_void_p]
-    done, t0 = 0, time.perf_counter()
-    passes = 0
-    while True:
-        if fn is not None:
-            fn(host.ctypes.data_as(C.c_void_p), sample_n, m, virgin.ctypes.data_as(C.c_void_p),
-               C.byref(last), hnb.ctypes.data_as(C.c_void_p), scratch.ctypes.data_as(C.c_void_p))
+    kind, fn = "port", None
+    if sfx and oracle.have_ref() and mode in (0, 1):
+        kind = "reference"
+        args7 = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p,
+                 C.c_void_p]
+        if mode == 1:
+            f = getattr(oracle.ref(), f"ref_dr_triage_loop_{sfx}")
+            f.argtypes = args7
+            fn = lambda: f(host.ctypes.data, sample_n, m, virgin.ctypes.data, C.byref(last),
+                           hnb.ctypes.data, scratch.ctypes.data)
         else:
-            kind = "port"
-            oracle.triage_batch(mode, host, None, threads=0)
+            f = getattr(oracle.ref(), f"ref_afl_triage_loop_{sfx}")
+            f.argtypes = args7
+            fn = lambda: f(host.ctypes.data, sample_n, m, oc.ctypes.data, virgin.ctypes.data,
+                           hnb.ctypes.data, scratch.ctypes.data)
+    if fn is None:
+        fn = lambda: oracle.triage_batch(mode, host, oc, threads=0)
+    done, passes, t0 = 0, 0, time.perf_counter()
+    while True:
+        fn()
         done += sample_n
         passes += 1
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": done / el, "unit": "traces/s", "cores": 1, "kind": kind,
+    return {"value": round(done / el, 1), "unit": "traces/s", "cores": 1, "kind": kind,
             "sample": f"{sample_n} traces x {m} B of the bench workload, {passes} sequential "
                       f"passes ({el:.1f} s), virgin carried, 1 thread"}
 
 
-def cpu_baseline_all_cores(traces_dev, mode, seconds):
-    """Clean-room restatement, exact sharded decomposition over all host cores (port)."""
+def cpu_baseline_all_cores(traces_dev, outcome_dev, mode, seconds):
+    """Clean-room restatement, exact sharded decomposition over the usable host cores (port):
+    two reads per trace (oracle/kbz_oracle.c kbzo_triage_batch_mt)."""
     import numpy as np
 
     import oracle
 
-    threads = min(os.cpu_count() or 1, 16)  # the GPU box's CPU share is 16 threads
-    sample_n = min(traces_dev.shape[0], 8192)
+    threads = usable_cores()
+    m = traces_dev.shape[1]
+    sample_n = min(traces_dev.shape[0], 16384 if m <= 65536 else 1024)
     host = traces_dev[:sample_n].cpu().numpy()
+    oc = outcome_dev[:sample_n].cpu().numpy().astype(np.int8)
     done, t0 = 0, time.perf_counter()
     while True:
-        oracle.triage_batch(mode, host, None, threads=threads)
+        oracle.triage_batch(mode, host, oc, threads=threads)
         done += sample_n
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": done / el, "unit": "traces/s", "cores": threads, "kind": "port",
-            "sample": f"{sample_n} traces, oracle/kbz_oracle.c kbzo_triage_batch_mt"}
+    return {"value": round(done / el, 1), "unit": "traces/s", "cores": threads, "kind": "port",
+            "sample": f"{sample_n} traces, oracle/kbz_oracle.c kbzo_triage_batch_mt, "
+                      f"{threads} threads (sched_getaffinity, cgroup quota)"}
 
 
-def main():
-    args = parse()
-    if args.workload == "merge":
-        return main_merge(args)
-    if args.workload == "stream":
-        return main_stream(args)
+# ---- roofline traffic (PMC) --------------------------------------------------------------------
+
+def _pmc_pass(counter, workload_args, outdir, timeout=240):
+    """One rocprofv3 --pmc pass over a short child run; per-dispatch values of `counter` for
+    the pass-1 kernel, in launch order."""
+    import csv
+    import glob
+
+    cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir, "-o", "run",
+           "--", sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-variants",
+           *workload_args]
+    subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=timeout,
+                   check=True)
+    vals = []
+    for f in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "k_pass1" in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
+                vals.append((int(r.get("Dispatch_Id", 0) or 0), float(r["Counter_Value"])))
+    return [v for _, v in sorted(vals)]
+
+
+def live_traffic(args, warmup=1, steps=4):
+    """HBM bytes per pass-1 launch from PMC (MI355X_MICROARCH.md HBM section): FETCH_SIZE and
+    WRITE_SIZE in separate passes (their TCC slots do not fit one pass), KiB per dispatch;
+    FETCH_SIZE doubled (gfx950 tallies 16 B/lane streaming reads at half their bytes).  The
+    median over the timed (fresh-batch) dispatches."""
+    import tempfile
+
+    wa = ["--workload", args.workload, "--mode", args.mode, "--batch", str(args.batch),
+          "--map-size", str(args.map_size), "--warmup", str(warmup), "--steps", str(steps),
+          "--seed", str(args.seed)]
+    with tempfile.TemporaryDirectory() as d:
+        fetch = _pmc_pass("FETCH_SIZE", wa, os.path.join(d, "f"))[warmup:]
+        write = _pmc_pass("WRITE_SIZE", wa, os.path.join(d, "w"))[warmup:]
+    if not fetch or not write:
+        return None
+    med = lambda v: sorted(v)[len(v) // 2]
+    return {"bytes": 2.0 * med(fetch) * 1024 + med(write) * 1024,
+            "source": f"live rocprofv3 --pmc, {len(fetch)} fresh-batch dispatches: "
+                      f"FETCH_SIZE x2 = {2.0 * med(fetch) * 1024:.0f} B + WRITE_SIZE = "
+                      f"{med(write) * 1024:.0f} B"}
+
+
+def stored_traffic(workload):
+    """The last committed PMC measurement for this workload (profiles/pass1_traffic*.json)."""
+    tf = os.path.join(ROOT, "profiles", "pass1_traffic.json" if workload == "config2"
+                      else f"pass1_traffic_{workload}.json")
+    try:
+        tj = json.load(open(tf))
+    except (OSError, ValueError):
+        return None
+    if tj.get("workload", "config2") != workload:
+        return None
+    return {"bytes": tj.get("hbm_bytes_per_launch"),
+            "source": f"stored PMC measurement {os.path.relpath(tf, ROOT)} "
+                      f"({tj.get('tag', 'earlier run')}), not this run"}
+
+
+# ---- triage workloads (config 2 / config 3) ----------------------------------------------------
+
+def main_triage(args):
     import torch
-    import torch.distributed as dist
 
     from killerbeez_amd import synth
     from killerbeez_amd.dist import triage_sharded
     from killerbeez_amd.triage import MODES, WANT_H32, TriageContext
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
-    torch.cuda.set_device(dev)
+    world, rank, dev = init_dist()
     mode = MODES[args.mode]
     B, M = args.batch, args.map_size
-
-    pool = []
-    gen = synth.dense_torch if args.workload == "config3" else synth.sparse_torch
-    for p in range(args.pool):
-        t, oc = gen(B, M, seed=args.seed + 7919 * p + 104729 * rank, device=dev)
-        pool.append((t, oc))
+    dense = args.workload == "config3"
+    gen = synth.dense_torch if dense else synth.sparse_torch
+    want_pool = args.pool or (args.warmup + args.steps)
+    free, _ = torch.cuda.mem_get_info(dev)
+    cap = max(2, int(0.6 * free) // (B * M))  # room left for the context and the variants
+    npool = max(2, min(want_pool, cap))
+    pool = [gen(B, M, seed=args.seed + 7919 * p + 104729 * rank, device=dev, hot_seed=args.seed)
+            for p in range(npool)]
     ctx = TriageContext(M, mode, B)
     out = {"hnb": torch.empty(B, dtype=torch.uint8, device=dev),
            "h32": torch.empty(B, dtype=torch.int32, device=dev)}
     counts = [B] * world
 
-    timings = []
-
-    def step(i, record=False):
-        t, oc = pool[i % len(pool)]
-        ctx._out = out
+    def step(t, oc):
         if world == 1:
-            ev = None
-            if record:
-                ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
-                ev[0].record()
             ctx.shard_begin(t, oc, WANT_H32, out=out)
-            if record:
-                ev[1].record()
-                timings.append(ev)
             ctx.shard_link(None, None, True, None, None)
             ctx.shard_reduce()
             ctx.shard_finish(None, None)  # single shard: its own aggregate is the total
         else:
-            ctx_out = triage_sharded(ctx, t, oc, counts, rank, world, WANT_H32, device=dev,
-                                     timings=timings if record else None)
-            del ctx_out
+            triage_sharded(ctx, t, oc, counts, rank, world, WANT_H32, device=dev)
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    ctx.sync()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i, record=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    ctx.sync()
-    if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-    pass1_ms = sum(a.elapsed_time(b) for a, b in timings) / max(1, len(timings))
-    total_traces = world * B * args.steps
-    value = total_traces / elapsed
+    def timed(batches, k):
+        """k steps over batches[i % len], bracketed by barrier + synchronize; max over ranks.
+        Returns (seconds, pass-1 ms per launch)."""
+        barrier_sync(world, dev)
+        ctx.sync()
+        ctx.time_pass1(True)
+        t0 = time.perf_counter()
+        for i in range(k):
+            step(*batches[i % len(batches)])
+        barrier_sync(world, dev)
+        el = time.perf_counter() - t0
+        ms, launches = ctx.time_pass1(False)
+        ctx.sync()
+        return max_over_ranks(el, world, dev), ms / max(1, launches)
+
+    # warmup on fresh batches (the first one on all-0xff virgin maps, timed by itself)
+    cold_s, _ = timed(pool[:1], 1)
+    for i in range(1, args.warmup):
+        step(*pool[i % npool])
+    fresh = pool[args.warmup:] if npool > args.warmup else pool
+    elapsed, pass1_ms = timed(fresh, args.steps)
+    n_fresh = min(args.steps, len(fresh))
+    value = world * B * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
     achieved = B * M / (pass1_ms * 1e-3) / 1e9  # GB/s, algorithmic bytes of one launch
+    variants = {"cold_first_batch_ms": round(1e3 * cold_s, 4)}
+    if not args.no_variants:
+        seen = pool[-2:]
+        el2, p2 = timed(seen, args.steps)
+        variants["steady_state_seen_batches"] = {
+            "value": round(world * B * args.steps / el2, 1),
+            "ms_per_step": round(1e3 * el2 / args.steps, 4), "pass1_ms": round(p2, 4),
+            "what": "the same steps re-triaging 2 already absorbed batches (nothing new)"}
+        if mode == MODES["dynamorio"]:
+            reps = 0
+            rb = fresh[:max(1, min(len(fresh), args.steps))]
+            for i, (t, oc) in enumerate(rb):
+                reps += synth.with_repeats_torch(t, oc, args.repeat_frac,
+                                                 seed=args.seed + 31 * i + rank)
+            el3, p3 = timed(rb, args.steps)
+            st = ctx.stats()
+            variants[f"repeats{int(round(100 * args.repeat_frac))}"] = {
+                "value": round(world * B * args.steps / el3, 1),
+                "ms_per_step": round(1e3 * el3 / args.steps, 4), "pass1_ms": round(p3, 4),
+                "rest_of_step_ms": round(1e3 * el3 / args.steps - p3, 4),
+                "repeated_execs": reps, "last_batch_fixed_chunks": st["fixed_chunks"],
+                "what": f"{len(rb)} of the fresh batches with {args.repeat_frac:.0%} of execs "
+                        "repeating their predecessor (last-hash skips), virgin carried"}
+    del pool, fresh
     traffic = None
-    # PMC bytes per launch measured for THIS workload's pass-1 kernel (scripts/pmc_traffic.py)
-    tf = os.path.join(ROOT, "profiles", "pass1_traffic.json" if args.workload == "config2"
-                      else f"pass1_traffic_{args.workload}.json")
-    if os.path.exists(tf):
+    if rank == 0 and world == 1 and args.pmc:
         try:
-            tj = json.load(open(tf))
-            if tj.get("workload", "config2") == args.workload:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+            traffic = live_traffic(args)
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal
+            traffic = {"bytes": None, "source": f"live PMC failed: {type(e).__name__}"}
+    if traffic is None:
+        traffic = stored_traffic(args.workload) or {"bytes": None, "source": "none"}
     res = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -225,141 +386,290 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": f"synthetic (SURVEY.md §8(d) {args.workload} generator, seeded, generated in HBM)",
-        "config": {"workload": f"{args.workload}: {B} "
-                               f"{'dense' if args.workload == 'config3' else 'sparse'} "
+        "data": f"synthetic (SURVEY.md §8(d) {args.workload} generator, seeded, generated in HBM; "
+                f"{n_fresh} distinct never-seen batches in the timed steps)",
+        "config": {"workload": f"{args.workload}: {B} {'dense' if dense else 'sparse'} "
                                f"traces/GPU x {M} B map, {args.mode} "
-                               "classify+hash32+last-hash skip+has_new_bits, virgin carried",
+                               "classify+hash32+last-hash skip+has_new_bits, virgin carried, "
+                               "fresh batches",
                    "map_size": M, "batch_per_gpu": B, "global_batch": world * B,
                    "mode": args.mode, "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": ("k_pass1w" if args.workload == "config3" else "k_pass1s"),
+                     "traffic": traffic["bytes"], "traffic_source": traffic["source"],
+                     "kernel": "k_pass1s" if B >= 512 * 64 else "k_pass1w",
                      "avg_launch_ms": round(pass1_ms, 4),
                      "algorithmic_bytes_per_launch": B * M},
         "pass1_share_of_step": round(pass1_ms / ms_per_step, 4),
+        "variants": variants,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(pool[0][0], mode, args.cpu_seconds)
-        res["cpu_baseline_all_cores"] = cpu_baseline_all_cores(pool[0][0], mode,
+        t0, oc0 = gen(min(B, 16384), M, seed=args.seed + 1, device=dev, hot_seed=args.seed)
+        res["cpu_baseline"] = cpu_baseline(t0, oc0, mode, args.cpu_seconds)
+        res["cpu_baseline_all_cores"] = cpu_baseline_all_cores(t0, oc0, mode,
                                                                max(2.0, args.cpu_seconds / 3))
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
+    finish(world)
 
 
-def _timed(fn, steps, warmup):
-    import torch
-
-    for _ in range(warmup):
-        fn()
-    torch.cuda.synchronize()
-    ev = []
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        fn()
-        b.record()
-        ev.append((a, b))
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    return el, sum(a.elapsed_time(b) for a, b in ev) / len(ev)
-
+# ---- config 4: merger --------------------------------------------------------------------------
 
 def main_merge(args):
     """BASELINE config 4: N client states (3 virgin maps of 64 KiB each) AND-folded into one
-    (merger/merger.c:79-99), states resident in HBM; one step = one fold of all N.  Each state
-    is all-0xff with random bits cleared (AND of 6 random bytes: P(clear) = 1/64)."""
+    (merger/merger.c:79-99), states resident in HBM, split evenly over the ranks (strong
+    scaling: the N states are the job); one step = one fold of all N (local fold, all-gather of
+    the partial folds, local AND: killerbeez_amd.dist.merge_sharded).  Each state is all-0xff
+    with random bits cleared (AND of 6 random bytes: P(clear) = 1/64)."""
     import torch
 
+    from killerbeez_amd.dist import merge_sharded, split_counts
     from killerbeez_amd.triage import merge_and
 
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
-    n, sb = args.states, 3 * 65536
+    world, rank, dev = init_dist()
+    n_all, sb = args.states, 3 * 65536
+    counts = split_counts(n_all, world)
+    n = counts[rank]
     states = torch.empty((n, sb), dtype=torch.uint8, device=dev)
     g = torch.Generator(device=dev)
-    g.manual_seed(args.seed)
-    for lo in range(0, n, 2000):
-        hi = min(n, lo + 2000)
-        clr = torch.randint(0, 256, (hi - lo, sb), dtype=torch.uint8, device=dev, generator=g)
+    g.manual_seed(args.seed + rank)
+    for a in range(0, n, 2000):
+        b = min(n, a + 2000)
+        clr = torch.randint(0, 256, (b - a, sb), dtype=torch.uint8, device=dev, generator=g)
         for _ in range(5):
-            clr &= torch.randint(0, 256, (hi - lo, sb), dtype=torch.uint8, device=dev,
-                                 generator=g)
-        states[lo:hi] = ~clr
+            clr &= torch.randint(0, 256, (b - a, sb), dtype=torch.uint8, device=dev, generator=g)
+        states[a:b] = ~clr
     out = torch.empty(sb, dtype=torch.uint8, device=dev)
-    el, ms = _timed(lambda: merge_and(states, out=out), args.steps, args.warmup)
-    torch.cuda.synchronize()
-    # size-independent property: the fold equals the AND of the folds of the two halves
-    halves = merge_and(states[: n // 2]) & merge_and(states[n // 2:])
-    if not torch.equal(halves, out):
-        raise SystemExit("merge self-check failed")
+    fold_ev = []
+
+    def step(record=False):
+        if record:
+            e = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+            e[0].record()
+        local = merge_and(states)
+        if record:
+            e[1].record()
+            fold_ev.append(e)
+        merge_sharded(local.view(1, sb), world, out=out)
+
+    for _ in range(args.warmup):
+        step()
+    barrier_sync(world, dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    barrier_sync(world, dev)
+    el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    ms = sum(a.elapsed_time(b) for a, b in fold_ev) / len(fold_ev)
+    if world == 1:  # size-independent property: the fold equals the AND of the halves' folds
+        halves = merge_and(states[: n // 2]) & merge_and(states[n // 2:])
+        if not torch.equal(halves, out):
+            raise SystemExit("merge self-check failed")
     bytes_ = n * sb
     res = {"metric": "merger states AND-folded/sec (3 x 64 KiB virgin maps per state)",
-           "value": round(n * args.steps / el, 1), "unit": "states/s", "n_gpus": 1,
+           "value": round(n_all * args.steps / el, 1), "unit": "states/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(1e3 * el / args.steps, 4), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+           "scaling": "strong", "vs_baseline": None, "dtype": "u8",
            "data": "synthetic merger states (all-0xff, bits cleared w.p. 1/64), generated in HBM",
-           "config": {"workload": f"config4: {n} states x {sb} B, one AND-fold per step",
-                      "states": n, "state_bytes": sb, "parallelism": "shard1"},
+           "config": {"workload": f"config4: {n_all} states x {sb} B over {world} GPU(s), one "
+                                  "AND-fold per step (local fold + all-gather + local AND)",
+                      "states": n_all, "state_bytes": sb, "parallelism": f"shard{world}"},
            "roofline": {"bound": "hbm", "achieved": round(bytes_ / (ms * 1e-3) / 1e9, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(bytes_ / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                        "traffic": None, "kernel": "k_and_groups + k_and_rows (one fold)",
+                        "traffic": None, "kernel": "k_and_groups + k_and_rows (one local fold)",
                         "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": bytes_}}
-    if not args.no_cpu:
-        import oracle
+    if rank == 0 and world == 1 and not args.no_cpu:
+        res["cpu_baseline"] = merge_cpu_baseline(states, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    finish(world)
 
-        sample = states[:2000].cpu().numpy()
-        done, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < args.cpu_seconds:
-            oracle.merge_many(sample)
-            done += sample.shape[0]
-        el_c = time.perf_counter() - t0
-        res["cpu_baseline"] = {"value": done / el_c, "unit": "states/s", "cores": 1,
-                               "kind": "port",
-                               "sample": f"2000 states of the workload, AND-folded repeatedly "
-                                         f"({el_c:.1f} s), oracle kbzo_merge_many, 1 thread"}
-    print(json.dumps(res), flush=True)
 
+def merge_cpu_baseline(states, seconds):
+    """The reference's own merge_bitmaps (afl_instrumentation.c:116-121) in the merger's fold
+    order (merger/merger.c:79-99 -> afl_merge :123-140; oracle/_ref ref_afl_merge_loop), one
+    core, on 2,000 states of the workload (JSON decode excluded: its encoding is external)."""
+    import ctypes as C
+
+    import numpy as np
+
+    import oracle
+
+    sample = states[:2000].cpu().numpy()
+    acc = np.full(sample.shape[1], 0xFF, np.uint8)
+    if oracle.have_ref():
+        f = oracle.ref().ref_afl_merge_loop_64k
+        f.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        fn, kind = (lambda: f(acc.ctypes.data, sample.ctypes.data, sample.shape[0])), "reference"
+    else:
+        fn, kind = (lambda: oracle.merge_many(sample)), "port"
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        fn()
+        done += sample.shape[0]
+    el = time.perf_counter() - t0
+    return {"value": round(done / el, 1), "unit": "states/s", "cores": 1, "kind": kind,
+            "sample": f"{sample.shape[0]} states of the workload AND-folded repeatedly "
+                      f"({el:.1f} s), merge_bitmaps in merger.c's fold order, 1 thread"}
+
+
+# ---- config 5: streaming ingest + unique crash/hang table --------------------------------------
 
 def main_stream(args):
-    """BASELINE config 5 (1 GPU): config-2 traces in pageable host memory, triaged through
-    kbz_triage_batch_host (pinned ring, double-buffered hipMemcpyAsync).  PCIe-bound; this is
-    the PCIe-inclusive rate DESIGN.md quotes, never the headline value."""
+    """BASELINE config 5: config-2 traces in pageable host memory, produced into the pinned
+    ingest ring (kbz_ring_acquire/submit: double-buffered hipMemcpyAsync, triage with XXH64)
+    and the crash/hang traces' keys {XXH64, outcome class} inserted into the unique crash/hang
+    table, replicated on every rank (killerbeez_amd.dist.dedup_sharded: all-gather of the keys
+    in global trace order).  PCIe-bound; `value` = traces/s over all ranks, host to results."""
+    import numpy as np
     import torch
 
     from killerbeez_amd import synth
-    from killerbeez_amd.triage import MODES, WANT_H32, TriageContext
+    from killerbeez_amd.dist import dedup_sharded
+    from killerbeez_amd.triage import MODES, WANT_H32, WANT_X64, TriageContext, UniqueSet
 
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
-    B, M = min(args.batch, 16384), args.map_size
-    t, oc = synth.sparse_torch(B, M, seed=args.seed, device=dev)
-    host, hoc = t.cpu().numpy(), oc.cpu().numpy()
+    world, rank, dev = init_dist()
+    M = args.map_size
+    t, oc = synth.sparse_torch(16384, M, seed=args.seed + 104729 * rank, device=dev,
+                               hot_seed=args.seed)
+    host, hoc = t.cpu().numpy(), oc.cpu().numpy().astype(np.int8)
     del t, oc
-    ctx = TriageContext(M, MODES[args.mode], B)
-    for _ in range(args.warmup):
-        ctx.triage_host(host, hoc, WANT_H32)
+    ctx = TriageContext(M, MODES[args.mode], min(args.batch, 4096))
+    table = UniqueSet(1 << 20)
+    rows, _ = ctx.ring_acquire()
+    slot = rows.shape[0]
+    ctx.ring_submit(0, False)
+    ctx.ring_flush()
+    pending = []  # (hnb, h32, x64, outcome) of submitted slots, filled on re-acquire / flush
+    n_new = 0
+
+    def dedup(item):
+        nonlocal n_new
+        _, _, x64, o = item
+        keys = torch.from_numpy(np.stack([x64.view(np.int64), o.astype(np.int64)], 1)).to(dev)
+        mask = torch.from_numpy(o != 0).to(dev)
+        n_new += int(dedup_sharded(table, keys, mask, rank, world).sum().item())
+
+    def step(i):
+        r, o = ctx.ring_acquire()  # waits for this slot's previous batch: its results are in
+        if len(pending) >= 2:
+            dedup(pending.pop(0))
+        lo = (i * slot) % (host.shape[0] - slot + 1)
+        r[:slot] = host[lo:lo + slot]
+        o[:slot] = hoc[lo:lo + slot]
+        res = (np.empty(slot, np.uint8), np.empty(slot, np.uint32), np.empty(slot, np.uint64),
+               hoc[lo:lo + slot].copy())
+        ctx.ring_submit(slot, True, res[0], res[1], res[2], WANT_H32 | WANT_X64)
+        pending.append(res)
+
+    def drain():
+        ctx.ring_flush()
+        while pending:
+            dedup(pending.pop(0))
+
+    for i in range(args.warmup):
+        step(i)
+    drain()
+    barrier_sync(world, dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ctx.triage_host(host, hoc, WANT_H32)
-    el = time.perf_counter() - t0
-    res = {"metric": "traces triaged/sec from host memory (64KB map, PCIe-inclusive)",
-           "value": round(B * args.steps / el, 1), "unit": "traces/s", "n_gpus": 1,
+    for i in range(args.steps):
+        step(args.warmup + i)
+    drain()
+    barrier_sync(world, dev)
+    el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    traces = world * slot * args.steps
+    res = {"metric": "traces triaged/sec from host memory (64KB map, PCIe-inclusive) + unique "
+                     "crash/hang table",
+           "value": round(traces / el, 1), "unit": "traces/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(1e3 * el / args.steps, 4), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
            "data": "synthetic config-2 traces in pageable host memory",
-           "config": {"workload": f"stream: {B} sparse traces x {M} B per step via the pinned "
-                                  "ring", "batch": B, "map_size": M, "mode": args.mode},
-           "pcie_GBps": round(B * M * args.steps / el / 1e9, 2)}
-    print(json.dumps(res), flush=True)
+           "config": {"workload": f"stream: {slot} sparse traces x {M} B per step and GPU via the "
+                                  "pinned ring, XXH64 keys of crash/hang traces into the "
+                                  "replicated unique table", "slot": slot, "map_size": M,
+                      "mode": args.mode, "parallelism": f"shard{world}"},
+           "pcie_GBps_per_gpu": round(slot * M * args.steps / el / 1e9, 2),
+           "unique_crash_hang_keys": table.size(), "new_keys_reported": n_new}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
     ctx.close()
+    finish(world)
+
+
+# ---- plugin per-exec latency -------------------------------------------------------------------
+
+def main_plugin(args):
+    """Per-exec latency of the instrumentation plugin (libkbz_plugin.so, include/kbz_plugin.h)
+    driven like fuzzer/main.c:370-418: every exec's raw trace is recorded, its novelty queried.
+    Batch 1 = the unmodified per-exec loop (is_new_path after each exec flushes a batch of one);
+    batch B = record B execs, then query their results (one GPU batch).  Reported next to the
+    reference's own per-exec step on one core (oracle/_ref)."""
+    import ctypes as C
+
+    import torch
+
+    from killerbeez_amd import build, synth
+
+    torch.cuda.set_device(0)
+    M = args.map_size
+    name = "dynamorio" if args.mode == "dynamorio" else "afl"
+    L = C.CDLL(build.PLUGIN_LIB)
+    create = getattr(L, f"kbz_{name}_gpu_create")
+    create.restype, create.argtypes = C.c_void_p, [C.c_char_p, C.c_char_p]
+    record = getattr(L, f"kbz_{name}_gpu_record")
+    record.restype, record.argtypes = C.c_long, [C.c_void_p, C.c_void_p, C.c_int]
+    result = getattr(L, f"kbz_{name}_gpu_result")
+    result.restype, result.argtypes = C.c_int, [C.c_void_p, C.c_long]
+    cleanup = getattr(L, f"kbz_{name}_gpu_cleanup")
+    cleanup.argtypes = [C.c_void_p]
+    t, oc = synth.sparse_np(8192, M, seed=args.seed)
+    if name == "dynamorio":
+        oc[:] = 0
+    per = {}
+    for bs in (1, 16, 256, 4096):
+        p = create(json.dumps({"map_size": M, "max_batch": bs}).encode(), None)
+        if not p:
+            raise SystemExit("plugin create failed")
+        total = 1024 if bs == 1 else 8192
+        for j in range(min(bs, 64)):  # warm: context, pinned slots
+            result(p, record(p, t[j].ctypes.data, int(oc[j])))
+        t0 = time.perf_counter()
+        done = 0
+        while done < total:
+            k = min(bs, total - done)
+            tickets = [record(p, t[(done + j) % 8192].ctypes.data, int(oc[(done + j) % 8192]))
+                       for j in range(k)]
+            for tk in tickets:
+                if result(p, tk) < 0:
+                    raise SystemExit("plugin result failed")
+            done += k
+        el = time.perf_counter() - t0
+        per[str(bs)] = round(1e6 * el / total, 3)
+        cleanup(p)
+    res = {"metric": "per-exec triage latency through the instrumentation plugin",
+           "value": per["1"], "unit": "us/exec", "n_gpus": 1, "steps": 1, "warmup": 1,
+           "higher_is_better": False, "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic config-2 traces in host memory",
+           "config": {"workload": f"plugin {name}_gpu: record + result per exec, batch sizes "
+                                  "1/16/256/4096", "map_size": M, "mode": args.mode},
+           "us_per_exec_by_batch": per}
+    if not args.no_cpu:
+        cb = cpu_baseline(torch.from_numpy(t), torch.from_numpy(oc),
+                          1 if name == "dynamorio" else 0, min(args.cpu_seconds, 5.0))
+        cb["us_per_exec"] = round(1e6 / cb["value"], 3)
+        res["cpu_baseline"] = cb
+    print(json.dumps(res), flush=True)
+
+
+def main():
+    args = parse()
+    maybe_launch(args)
+    {"merge": main_merge, "stream": main_stream, "plugin": main_plugin}.get(
+        args.workload, main_triage)(args)
 
 
 if __name__ == "__main__":

@@ -103,6 +103,11 @@ int kbz_ctx_set_pass1(kbz_ctx_t *ctx, int choice);
  * coverage found), chunks recomputed by the DynamoRIO skip fix path, DynamoRIO skipped rows that
  * differ from their predecessor (hash collisions).  Synchronous; diagnostics only. */
 int kbz_ctx_stats(kbz_ctx_t *ctx, uint32_t *out);
+/* Timing of the dominant kernel (pass 1) with HIP events recorded around each of its launches on
+ * the launch stream.  Returns the summed duration (ms) and count of the launches timed since
+ * the previous call (waiting for them), then enables (enable != 0) or disables timing of later
+ * launches.  Diagnostics only (bench.py's roofline). */
+int kbz_ctx_time_pass1(kbz_ctx_t *ctx, int enable, double *total_ms, uint32_t *launches);
 
 /* ---- batched triage ------------------------------------------------------------------------ */
 /* traces:   device, n rows of map_size raw 8-bit hit counters, row j at traces + j*stride

@@ -1513,6 +1513,10 @@ struct kbz_ctx {
   } ring[2];
   int ring_next = 0;        // slot the next kbz_ring_acquire returns
   int ring_acquired = -1;   // slot handed out and not yet submitted
+  // kbz_ctx_time_pass1: HIP events around every pass-1 launch (on its stream)
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pass1;
+  size_t ev_used_n = 0;
 };
 
 namespace {
@@ -1571,6 +1575,10 @@ void free_ctx(kbz_ctx *c) {
     if (c->pin_oc[i]) (void)hipHostFree(c->pin_oc[i]);
     if (c->ev_copied[i]) (void)hipEventDestroy(c->ev_copied[i]);
     if (c->ev_used[i]) (void)hipEventDestroy(c->ev_used[i]);
+  }
+  for (auto &e : c->ev_pass1) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
   }
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->work_stream) (void)hipStreamDestroy(c->work_stream);
@@ -1785,6 +1793,22 @@ int kbz_ctx_stats(kbz_ctx_t *c, uint32_t *out) {
   HIP_TRY(hipMemcpy(out, c->counters + 8, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost));
   return 0;
 }
+int kbz_ctx_time_pass1(kbz_ctx_t *c, int enable, double *total_ms, uint32_t *launches) {
+  if (!c) return fail("null ctx");
+  DevGuard g(c->device);
+  double sum = 0;
+  for (size_t i = 0; i < c->ev_used_n; i++) {
+    HIP_TRY(hipEventSynchronize(c->ev_pass1[i].second));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev_pass1[i].first, c->ev_pass1[i].second));
+    sum += ms;
+  }
+  if (total_ms) *total_ms = sum;
+  if (launches) *launches = (uint32_t)c->ev_used_n;
+  c->ev_used_n = 0;
+  c->timing = enable != 0;
+  return 0;
+}
 int kbz_ctx_set_pass1(kbz_ctx_t *c, int choice) {
   if (!c) return fail("null ctx");
   if (choice < KBZ_PASS1_AUTO || choice > KBZ_PASS1_WIDE) return fail("bad pass-1 choice");
@@ -1848,7 +1872,19 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
   a.vcur = c->V[c->vcur];
   a.tflags = c->tflags;
   a.nfw = c->nfw;
+  hipEvent_t *ev = nullptr;
+  if (c->timing) {
+    if (c->ev_used_n == c->ev_pass1.size()) {
+      std::pair<hipEvent_t, hipEvent_t> e;
+      HIP_TRY(hipEventCreate(&e.first));
+      HIP_TRY(hipEventCreate(&e.second));
+      c->ev_pass1.push_back(e);
+    }
+    ev = &c->ev_pass1[c->ev_used_n++].first;
+    HIP_TRY(hipEventRecord(ev[0], s));
+  }
   if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, s)) return -1;
+  if (ev) HIP_TRY(hipEventRecord(c->ev_pass1[c->ev_used_n - 1].second, s));
   if (c->mode == KBZ_MODE_DYNAMORIO) {  // the skip rule for rows j >= 1 needs no other shard
     hipLaunchKernelGGL(k_skip, dim3(cdiv(n, 256)), dim3(256), 0, s, c->cur_h32, c->neq,
                        (uint32_t)n, c->skip, c->flags, c->fix_list, c->counters + 3, c->bad_list,
@@ -2301,6 +2337,30 @@ int kbz_merge_and_device(uint8_t *out, const uint8_t *states, size_t n, size_t s
   return 0;
 }
 
+namespace {
+// Resources of one kbz_merge_and_host call, released on every exit path.
+struct MergeStaging {
+  hipStream_t cs = nullptr, ws = nullptr;
+  uint8_t *pin[2] = {nullptr, nullptr}, *dst[2] = {nullptr, nullptr};
+  uint8_t *acc = nullptr, *part = nullptr;
+  hipEvent_t copied[2] = {nullptr, nullptr}, used[2] = {nullptr, nullptr};
+  ~MergeStaging() {
+    if (ws) (void)hipStreamSynchronize(ws);
+    if (cs) (void)hipStreamSynchronize(cs);
+    for (int i = 0; i < 2; i++) {
+      if (pin[i]) (void)hipHostFree(pin[i]);
+      if (dst[i]) (void)hipFree(dst[i]);
+      if (copied[i]) (void)hipEventDestroy(copied[i]);
+      if (used[i]) (void)hipEventDestroy(used[i]);
+    }
+    if (acc) (void)hipFree(acc);
+    if (part) (void)hipFree(part);
+    if (cs) (void)hipStreamDestroy(cs);
+    if (ws) (void)hipStreamDestroy(ws);
+  }
+};
+}  // namespace
+
 int kbz_merge_and_host(uint8_t *out, const uint8_t *states, size_t n, size_t state_bytes) {
   if (!out || (!states && n)) return fail("null argument");
   if (state_bytes == 0) return 0;
@@ -2309,56 +2369,41 @@ int kbz_merge_and_host(uint8_t *out, const uint8_t *states, size_t n, size_t sta
     return 0;
   }
   const size_t per = std::max<size_t>(1, (256u << 20) / state_bytes);
-  hipStream_t cs, ws;
-  HIP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&ws, hipStreamNonBlocking));
-  uint8_t *pin[2] = {nullptr, nullptr}, *dst[2] = {nullptr, nullptr}, *acc = nullptr,
-          *part = nullptr;
-  hipEvent_t copied[2], used[2];
   const size_t cap = std::min(per, n);
+  MergeStaging m;
+  HIP_TRY(hipStreamCreateWithFlags(&m.cs, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&m.ws, hipStreamNonBlocking));
   for (int i = 0; i < 2; i++) {
-    HIP_TRY(hipHostMalloc((void **)&pin[i], cap * state_bytes, hipHostMallocDefault));
-    HIP_TRY(hipMalloc((void **)&dst[i], cap * state_bytes));
-    HIP_TRY(hipEventCreateWithFlags(&copied[i], hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&used[i], hipEventDisableTiming));
+    HIP_TRY(hipHostMalloc((void **)&m.pin[i], cap * state_bytes, hipHostMallocDefault));
+    HIP_TRY(hipMalloc((void **)&m.dst[i], cap * state_bytes));
+    HIP_TRY(hipEventCreateWithFlags(&m.copied[i], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&m.used[i], hipEventDisableTiming));
   }
-  HIP_TRY(hipMalloc((void **)&acc, state_bytes));
-  HIP_TRY(hipMalloc((void **)&part, state_bytes));
-  HIP_TRY(hipMemsetAsync(acc, 0xff, state_bytes, ws));
-  int rc = 0;
+  HIP_TRY(hipMalloc((void **)&m.acc, state_bytes));
+  HIP_TRY(hipMalloc((void **)&m.part, state_bytes));
+  HIP_TRY(hipMemsetAsync(m.acc, 0xff, state_bytes, m.ws));
   for (size_t lo = 0, b = 0; lo < n; lo += cap, b++) {
     const int sl = (int)(b & 1);
     const size_t cnt = std::min(cap, n - lo);
-    HIP_TRY(hipEventSynchronize(used[sl]));
-    memcpy(pin[sl], states + lo * state_bytes, cnt * state_bytes);
-    HIP_TRY(hipMemcpyAsync(dst[sl], pin[sl], cnt * state_bytes, hipMemcpyHostToDevice, cs));
-    HIP_TRY(hipEventRecord(copied[sl], cs));
-    HIP_TRY(hipStreamWaitEvent(ws, copied[sl], 0));
-    if ((rc = kbz_merge_and_device(part, dst[sl], cnt, state_bytes, ws))) break;
+    HIP_TRY(hipEventSynchronize(m.used[sl]));
+    memcpy(m.pin[sl], states + lo * state_bytes, cnt * state_bytes);
+    HIP_TRY(hipMemcpyAsync(m.dst[sl], m.pin[sl], cnt * state_bytes, hipMemcpyHostToDevice, m.cs));
+    HIP_TRY(hipEventRecord(m.copied[sl], m.cs));
+    HIP_TRY(hipStreamWaitEvent(m.ws, m.copied[sl], 0));
+    if (kbz_merge_and_device(m.part, m.dst[sl], cnt, state_bytes, m.ws)) return -1;
     if (state_bytes % 16 == 0) {
-      hipLaunchKernelGGL(k_and_rows, dim3(cdiv(state_bytes / 16, 256)), dim3(256), 0, ws, part,
-                         (size_t)1, state_bytes, acc, 1);
+      hipLaunchKernelGGL(k_and_rows, dim3(cdiv(state_bytes / 16, 256)), dim3(256), 0, m.ws, m.part,
+                         (size_t)1, state_bytes, m.acc, 1);
     } else {
-      hipLaunchKernelGGL(k_and_bytes, dim3(cdiv(state_bytes, 256)), dim3(256), 0, ws, part,
-                         (size_t)1, state_bytes, acc, 1);
+      hipLaunchKernelGGL(k_and_bytes, dim3(cdiv(state_bytes, 256)), dim3(256), 0, m.ws, m.part,
+                         (size_t)1, state_bytes, m.acc, 1);
     }
-    HIP_TRY(hipEventRecord(used[sl], ws));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(m.used[sl], m.ws));
   }
-  if (!rc) {
-    HIP_TRY(hipStreamSynchronize(ws));
-    HIP_TRY(hipMemcpy(out, acc, state_bytes, hipMemcpyDeviceToHost));
-  }
-  for (int i = 0; i < 2; i++) {
-    (void)hipHostFree(pin[i]);
-    (void)hipFree(dst[i]);
-    (void)hipEventDestroy(copied[i]);
-    (void)hipEventDestroy(used[i]);
-  }
-  (void)hipFree(acc);
-  (void)hipFree(part);
-  (void)hipStreamDestroy(cs);
-  (void)hipStreamDestroy(ws);
-  return rc;
+  HIP_TRY(hipStreamSynchronize(m.ws));
+  HIP_TRY(hipMemcpy(out, m.acc, state_bytes, hipMemcpyDeviceToHost));
+  return 0;
 }
 
 // ---- standalone hashes ---------------------------------------------------------------------------

@@ -81,3 +81,59 @@ def triage_sharded(engine, traces, outcome, counts, rank, world, want=1, group=N
     else:
         total, prefix = agg, None
     return engine.shard_finish(prefix, total)
+
+
+# ---- merger across GPUs (BASELINE config 4) ----------------------------------
+
+def merge_sharded(states, world, group=None, fold=None, out=None):
+    """The merger's AND-fold (merger/merger.c:79-99 -> afl_merge afl_instrumentation.c:123-140)
+    over states spread across ranks: every rank folds its own states (rows of `states`, any
+    count, possibly 0) with one local AND-fold, the ranks all-gather their partial folds
+    (state_bytes each, over xGMI), and every rank ANDs the world partials.  AND is associative
+    and commutative, so the result equals the sequential fold of all states in any order.
+    `fold(rows, out=None)` is the local AND-fold (default: kbz_merge_and_device); RCCL has no
+    bitwise-AND reduction, hence all-gather + local fold.  Returns the merged state (every
+    rank holds it)."""
+    if fold is None:
+        from .triage import merge_and as fold
+    local = fold(states)
+    if world == 1:
+        if out is not None:
+            out.copy_(local)
+            return out
+        return local
+    parts = _all_gather(local.contiguous(), world, group)
+    return fold(parts, out=out)
+
+
+# ---- unique crash/hang table across GPUs (BASELINE config 5; SURVEY.md §8(e)) ----------------
+
+def dedup_sharded(table, keys, mask, rank, world, group=None):
+    """The reference's insert-if-absent set novelty (linux_ipt_instrumentation.c:412-424: new iff
+    the key was absent; HASH_ADD keeps insertion order) over a batch sharded by contiguous trace
+    index.  keys: this rank's [n_r, 2] int64 keys (e.g. {XXH64 of the transformed trace,
+    outcome class}: triage.dedup_keys); mask: [n_r] bool/uint8, rows that take part (crash and
+    hang traces).  The masked keys of all ranks are all-gathered in rank order -- i.e. in global
+    trace order, with their global position implicit in that order -- and inserted as ONE
+    ordered batch into every rank's replica `table` (any object with UniqueSet.insert), so all
+    replicas stay identical and the first occurrence in global order is the new one.  Returns
+    this rank's is_new [n_r] uint8 (0 for masked-out rows)."""
+    dev = keys.device
+    m = mask.to(torch.bool)
+    sel = keys[m].contiguous()
+    if world > 1:
+        cnt = torch.tensor([sel.shape[0]], dtype=torch.int64, device=dev)
+        cnts = _all_gather(cnt, world, group).view(-1).tolist()
+        mx = max(cnts)
+        pad = torch.zeros((mx, 2), dtype=keys.dtype, device=dev)
+        pad[:sel.shape[0]] = sel
+        allk = _all_gather(pad, world, group)  # [world, mx, 2]
+        glob = torch.cat([allk[r, :cnts[r]] for r in range(world)]) if sum(cnts) else pad[:0]
+        off = sum(cnts[:rank])
+    else:
+        glob, off = sel, 0
+    isnew_all = table.insert(glob) if glob.shape[0] else torch.zeros(0, dtype=torch.uint8,
+                                                                     device=dev)
+    out = torch.zeros(keys.shape[0], dtype=torch.uint8, device=dev)
+    out[m] = isnew_all[off:off + sel.shape[0]].to(torch.uint8)
+    return out

@@ -63,15 +63,21 @@ def uniform_np(n, map_size=65536, seed=0, density=0.02):
 
 def sparse_torch(n, map_size=65536, seed=0x5EED, device="cuda", hot_frac=0.02, p_hot=0.9,
                  geo_p=0.35, cold_rate=0.5, uniform_counts=False, outcome_p=OUTCOME_P,
-                 out=None, block=4096):
+                 out=None, block=4096, hot_seed=None):
     """Same distribution generated directly in device memory (bench inputs, HBM-resident).
-    Returns (traces uint8 [n, M] on device, outcome int8 [n] on device)."""
+    hot_seed: seed of the hot edge set alone (batches of one target program share it; default:
+    drawn from `seed`).  Returns (traces uint8 [n, M] on device, outcome int8 [n] on device)."""
     import torch
 
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     H = max(1, int(round(hot_frac * map_size)))
-    hot = torch.randperm(map_size, generator=g, device=device)[:H]
+    if hot_seed is None:
+        hot = torch.randperm(map_size, generator=g, device=device)[:H]
+    else:
+        gh = torch.Generator(device=device)
+        gh.manual_seed(hot_seed)
+        hot = torch.randperm(map_size, generator=gh, device=device)[:H]
     t = out if out is not None else torch.empty((n, map_size), dtype=torch.uint8, device=device)
     t.zero_()
     lg = math.log1p(-geo_p)
@@ -115,3 +121,24 @@ def merger_states_np(n_states, map_size=65536, seed=0, clear_p=0.02):
     bits = rng.random((n_states, 3 * map_size, 8)) < clear_p
     clear = np.packbits(bits, axis=-1, bitorder="little")[..., 0]
     return s & ~clear
+
+
+def with_repeats_torch(traces, outcome, frac=0.9, seed=0):
+    """In place: every exec after the first repeats its predecessor (same trace, same outcome)
+    with probability `frac` -- the runs of identical execs of real fuzzing, where most mutations
+    do not change the path (the DynamoRIO last-hash skip's workload).  Returns the number of
+    repeated rows."""
+    import torch
+
+    n = traces.shape[0]
+    if n < 2:
+        return 0
+    g = torch.Generator(device=traces.device)
+    g.manual_seed(seed)
+    rep = torch.rand(n, generator=g, device=traces.device) < frac
+    rep[0] = False
+    idx = torch.arange(n, device=traces.device)
+    src = torch.cummax(torch.where(rep, torch.zeros_like(idx), idx), 0).values
+    traces.copy_(traces[src])
+    outcome.copy_(outcome[src])
+    return int(rep.sum().item())

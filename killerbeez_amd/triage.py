@@ -67,6 +67,14 @@ class TriageContext:
         check(lib().kbz_ctx_stats(self._h, _np_ptr(out)), "kbz_ctx_stats")
         return {"claims": int(out[0]), "fixed_chunks": int(out[1]), "bad_rows": int(out[2])}
 
+    def time_pass1(self, enable: bool = True):
+        """-> (summed ms, launches) of the pass-1 launches timed since the last call (HIP events
+        around each launch); then times later launches iff `enable`."""
+        ms, k = C.c_double(), C.c_uint32()
+        check(lib().kbz_ctx_time_pass1(self._h, int(bool(enable)), C.byref(ms), C.byref(k)),
+              "kbz_ctx_time_pass1")
+        return ms.value, k.value
+
     # -- lifetime --------------------------------------------------------------------------
     def close(self):
         if getattr(self, "_h", None):
@@ -143,6 +151,8 @@ class TriageContext:
         oc = None
         if outcome is not None:
             oc = outcome.to(device=dev, dtype=torch.int8).contiguous()
+            if stream is not None:  # the kernels read it on `stream` after this returns
+                oc.record_stream(stream)
         rc = lib().kbz_triage_batch_device(
             self._h, C.c_void_p(traces.data_ptr()), n, stride,
             None if oc is None else C.c_void_p(oc.data_ptr()),
@@ -207,6 +217,8 @@ class TriageContext:
             if want & WANT_X64:
                 out["x64"] = torch.empty(n, dtype=torch.int64, device=dev)
         self._oc = None if outcome is None else outcome.to(device=dev, dtype=torch.int8).contiguous()
+        if self._oc is not None and stream is not None:
+            self._oc.record_stream(stream)
         self._out = out
         rc = lib().kbz_shard_begin(
             self._h, C.c_void_p(traces.data_ptr()) if n else None, n, stride,
@@ -268,7 +280,7 @@ def merge_and(states, out=None, stream=None):
     import torch
 
     n = states.shape[0]
-    nbytes = states[0].numel() if n else 0
+    nbytes = states.shape[1] if states.dim() == 2 else (states[0].numel() if n else 0)
     if out is None:
         out = torch.empty(nbytes, dtype=torch.uint8, device=states.device)
     check(lib().kbz_merge_and_device(C.c_void_p(out.data_ptr()),
@@ -298,7 +310,12 @@ def triage_modules(ctxs, traces, offsets, outcome=None, stream=None):
     offs = (C.c_size_t * max(k, 1))(*offsets)
     hnb = torch.empty((k, n), dtype=torch.uint8, device=traces.device)
     anyv = torch.empty(n, dtype=torch.uint8, device=traces.device)
-    oc = None if outcome is None else C.c_void_p(outcome.data_ptr())
+    oct = None
+    if outcome is not None:  # device int8, alive until the kernels on `stream` have read it
+        oct = outcome.to(device=traces.device, dtype=torch.int8).contiguous()
+        if stream is not None:
+            oct.record_stream(stream)
+    oc = None if oct is None else C.c_void_p(oct.data_ptr())
     check(lib().kbz_triage_modules_device(hs, k, C.c_void_p(traces.data_ptr()) if n else None,
                                           n, traces.stride(0), offs, oc,
                                           C.c_void_p(hnb.data_ptr()) if n else None,
