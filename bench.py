@@ -317,23 +317,27 @@ def main_triage(args):
         else:
             triage_sharded(ctx, t, oc, counts, rank, world, WANT_H32, device=dev)
 
-    def timed(batches, k):
+    def timed(batches, k, events=False):
         """k steps over batches[i % len], bracketed by barrier + synchronize; max over ranks.
-        Returns (seconds, pass-1 ms per launch)."""
+        Returns (seconds, pass-1 ms per launch[, device ms of the k steps])."""
         barrier_sync(world, dev)
         ctx.sync()
         ctx.time_pass1(True)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         t0 = time.perf_counter()
+        ev[0].record()
         for i in range(k):
             step(*batches[i % len(batches)])
+        ev[1].record()
         barrier_sync(world, dev)
         el = time.perf_counter() - t0
         ms, launches = ctx.time_pass1(False)
         ctx.sync()
-        return max_over_ranks(el, world, dev), ms / max(1, launches)
+        r = (max_over_ranks(el, world, dev), ms / max(1, launches))
+        return r + (ev[0].elapsed_time(ev[1]),) if events else r
 
     # warmup on fresh batches (the first one on all-0xff virgin maps, timed by itself)
-    cold_s, _ = timed(pool[:1], 1)
+    _, _, cold_ms = timed(pool[:1], 1, events=True)
     for i in range(1, args.warmup):
         step(*pool[i % npool])
     fresh = pool[args.warmup:] if npool > args.warmup else pool
@@ -342,7 +346,7 @@ def main_triage(args):
     value = world * B * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
     achieved = B * M / (pass1_ms * 1e-3) / 1e9  # GB/s, algorithmic bytes of one launch
-    variants = {"cold_first_batch_ms": round(1e3 * cold_s, 4)}
+    variants = {"cold_first_batch_ms": round(cold_ms, 4)}
     if not args.no_variants:
         seen = pool[-2:]
         el2, p2 = timed(seen, args.steps)
@@ -558,7 +562,7 @@ def main_stream(args):
         if len(pending) >= 2:
             dedup(pending.pop(0))
         lo = (i * slot) % (host.shape[0] - slot + 1)
-        r[:slot] = host[lo:lo + slot]
+        torch.from_numpy(r[:slot]).copy_(torch.from_numpy(host[lo:lo + slot]))  # threaded
         o[:slot] = hoc[lo:lo + slot]
         res = (np.empty(slot, np.uint8), np.empty(slot, np.uint32), np.empty(slot, np.uint64),
                hoc[lo:lo + slot].copy())

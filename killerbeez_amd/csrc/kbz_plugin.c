@@ -51,10 +51,11 @@ typedef struct kbz_plugin {
   uint32_t last_hash;      /* dynamorio last_shm_hash */
   int mirror_stale;        /* the GPU copy is newer than the mirror */
   kbz_ctx_t *ctx;          /* GPU context, created on the first triage */
-  uint8_t *q_traces;       /* deferred execs, max_batch rows */
+  uint8_t *q_rows;         /* deferred execs: the acquired pinned ring slot (kbz_ring_acquire) */
   int8_t *q_outcome;
+  size_t q_cap;            /* its rows (<= max_batch) */
   size_t q_n;
-  long q_base;             /* ticket of q_traces[0] */
+  long q_base;             /* ticket of q_rows[0] */
   uint8_t *r_hnb;          /* results of the last flushed window */
   size_t r_n;
   long r_base;
@@ -140,8 +141,6 @@ static void plugin_free(kbz_plugin_t *p) {
   if (p->ctx) kbz_ctx_destroy(p->ctx);
   free(p->ignore);
   free(p->virgin);
-  free(p->q_traces);
-  free(p->q_outcome);
   free(p->r_hnb);
   free(p);
 }
@@ -155,10 +154,8 @@ static kbz_plugin_t *plugin_alloc(int mode, size_t map_size, size_t max_batch) {
   p->last_ticket = -1;
   p->last_fuzz_result = KBZ_PLUGIN_FUZZ_ERROR;
   p->virgin = (uint8_t *)malloc(3 * map_size);
-  p->q_traces = (uint8_t *)malloc(max_batch * map_size);
-  p->q_outcome = (int8_t *)malloc(max_batch);
   p->r_hnb = (uint8_t *)malloc(max_batch);
-  if (!p->virgin || !p->q_traces || !p->q_outcome || !p->r_hnb) {
+  if (!p->virgin || !p->r_hnb) {
     plugin_free(p);
     set_err("out of host memory");
     return NULL;
@@ -255,19 +252,21 @@ static int sync_mirror(kbz_plugin_t *p) {
   return 0;
 }
 
+/* Triage the queued execs (the acquired ring slot) as one ordered batch and wait for it.  A
+ * batch of at most 64 execs is read by the GPU straight from the pinned slot (no DMA). */
 static int plugin_flush(kbz_plugin_t *p) {
-  if (!p->q_n) return 0;
-  if (ensure_ctx(p)) return -1;
+  if (!p->q_rows) return 0;
   p->mirror_stale = 1;
-  if (kbz_triage_batch_host(p->ctx, p->q_traces, p->q_n, p->map_size, p->q_outcome, p->r_hnb,
-                            NULL, NULL, 0)) {
+  const size_t n = p->q_n;
+  p->q_rows = NULL;
+  p->q_n = 0;
+  if (kbz_ring_submit(p->ctx, n, 1, p->r_hnb, NULL, NULL, 0) || kbz_ring_flush(p->ctx)) {
     set_err("GPU triage: %s", kbz_last_error());
     return -1;
   }
   p->r_base = p->q_base;
-  p->r_n = p->q_n;
-  p->q_base += (long)p->q_n;
-  p->q_n = 0;
+  p->r_n = n;
+  p->q_base += (long)n;
   return 0;
 }
 
@@ -281,8 +280,17 @@ static long plugin_record(kbz_plugin_t *p, const uint8_t *trace, int fuzz_result
     set_err("fuzz_result must be FUZZ_NONE, FUZZ_HANG or FUZZ_CRASH");
     return -1;
   }
-  if (p->q_n == p->max_batch && plugin_flush(p)) return -1;
-  memcpy(p->q_traces + p->q_n * p->map_size, trace, p->map_size);
+  if (p->q_rows && p->q_n == p->q_cap && plugin_flush(p)) return -1;
+  if (!p->q_rows) {  /* the exec's trace goes straight into pinned memory */
+    if (ensure_ctx(p)) return -1;
+    if (kbz_ring_acquire(p->ctx, &p->q_rows, &p->q_outcome, &p->q_cap)) {
+      p->q_rows = NULL;
+      set_err("GPU ring: %s", kbz_last_error());
+      return -1;
+    }
+    if (p->q_cap > p->max_batch) p->q_cap = p->max_batch;
+  }
+  memcpy(p->q_rows + p->q_n * p->map_size, trace, p->map_size);
   /* the KBZ_FUZZ_* outcomes of kbz_triage.h use the same numbering */
   p->q_outcome[p->q_n] = (int8_t)fuzz_result;
   p->last_ticket = p->q_base + (long)p->q_n++;

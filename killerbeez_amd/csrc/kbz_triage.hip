@@ -405,30 +405,22 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
     const uint32_t seg = chunk / a.seg_len;
     // Virgin words of each tile travel with its rows: a 9th ring register per slot (lane l < 16 NC
     // loads 16 B of class l / 16), stored to a per-buffer LDS area next to the tile, so T can
-    // limit its stores to words that still hold virgin bits (below).  DynamoRIO (NC = 1): lanes
-    // 16-31 load the tile's 256 B of the PREVIOUS chunk's last row into the same area, so row 0
-    // (lane 0, which has no predecessor inside the wave) gets an exact neighbour test too.
-    // Chunk 0 has no previous row here (its row 0 is compared with the previous batch's or
-    // shard's last row by k_skip); it re-loads its own row 0 and ignores it.
+    // limit its stores to words that still hold virgin bits (below).
     u32x4 R[D][NLD + 1];
-    constexpr int NXL = (MODE == KBZ_MODE_DYNAMORIO) ? 32 : 16 * NC;  // lanes with a 9th load
     const uint32_t vl = min(lane, 16 * NC - 1);
-    const uint8_t *xbase = a.vcur + (size_t)(vl / 16) * a.map_size + (vl % 16) * 16;
-    if (MODE == KBZ_MODE_DYNAMORIO && lane >= 16 && lane < 32)
-      xbase = a.traces + (row0 ? row0 - 1 : 0) * a.stride + (lane - 16) * 16;
+    const uint8_t *vbase = a.vcur + (size_t)(vl / 16) * a.map_size + (vl % 16) * 16;
     auto load_t = [&](u32x4 (&r)[NLD + 1], uint32_t t) {
       load_half(*(u32x4(*)[NLD])r, t);
       const uint32_t msk = t < ntiles ? ~0u : 0u;
-      asm_load16_cached(r[NLD], xbase + ((t * TW) & msk));
+      asm_load16_cached(r[NLD], vbase + ((t * TW) & msk));
     };
     auto store_t = [&](const u32x4 (&r)[NLD + 1], int b) {
       store_half(*(const u32x4(*)[NLD])r, b);
-      if (lane < NXL) {
+      if (lane < 16 * NC) {
         const u32x4 v = r[NLD];
         lds[2 * TILE + b * 48 + lane] = make_uint4(v.x, v.y, v.z, v.w);
       }
     };
-    bool neq0 = false;  // DynamoRIO, chunk > 0: row 0 differs from the previous chunk's last row
 #pragma unroll
     for (int d = 0; d < D; d++) load_t(R[d], d);
     uint64_t tfl[NC];  // stored-tile bits of the current 64-tile flag word
@@ -479,17 +471,6 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         // raw AFL words are their own transform (only simplified lanes change)
         if (dirty && (MODE != KBZ_MODE_AFL || simp)) *slot = v;
       }
-      if (MODE == KBZ_MODE_DYNAMORIO && chunk > 0 && !(ABL & 1)) {
-        // row 0 (transformed in place above; all-zero columns stay 0 == classify(0)) against
-        // the previous chunk's last row, word `lane` of this tile, on the examined bytes
-        uint64_t d = 0;
-        if (lane < TW / 8) {
-          const uint64_t pw = classify8(((const uint64_t *)&lds[2 * TILE + b * 48 + 16])[lane]);
-          const uint64_t cw = ((const uint64_t *)&lds[b * TILE + (lane >> 1)])[lane & 1];
-          d = (pw ^ cw) & (IGN ? ~nonzero_bytes8(ig[lane]) : ~0ull);
-        }
-        neq0 |= __ballot(d != 0) != 0;
-      }
       // chunk_or keeps only bits still virgin at batch entry (orw & V): the scan uses nothing
       // else (its new bits are o & V & ~prev, and f2 only looks at bytes with V == 0xff), and a
       // tile with none is not stored at all, only its flag bit stays clear.  In steady-state
@@ -536,7 +517,9 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
     }
     KBZ_STAMP_FLUSH(chunk * 2 + 1);
     drain_asm_loads(R);
-    if (MODE == KBZ_MODE_DYNAMORIO && valid) a.neq[row0 + lane] = (lane == 0 && chunk > 0) ? neq0 : neq != 0;
+    // lane 0 has no predecessor in the wave: its value is a placeholder (k_skip compares a chunk's
+    // row 0 with the previous row itself, and only when their hashes are equal)
+    if (MODE == KBZ_MODE_DYNAMORIO && valid) a.neq[row0 + lane] = neq != 0;
   }
 }
 
@@ -571,14 +554,12 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
   static_assert(kChunk % (2 * NX) == 0, "equal row groups");
   constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, RPW = kChunk / NL, NLD = RPW / RPI;
-  constexpr int NE = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 0;  // extra loads per tile (prev row)
   constexpr int TILE = kChunk * SLOTS;  // uint4 per tile buffer
   constexpr int RG = kChunk / (2 * NX);  // rows per X row group
   __shared__ uint4 lds[3 * TILE];
   __shared__ uint4 kbuf[3 * TILE];             // k of each (row, word), same layout as lds
   __shared__ uint64_t orb[3][NC][TW / 8];      // column ORs of the tile, per class
   __shared__ uint64_t bnd[2][2 * NX][TW / 8];  // last row of each group (neighbour test)
-  __shared__ uint64_t prv[3][TW / 8];          // DynamoRIO: previous chunk's last row, raw
   __shared__ uint64_t neqs[NX];
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -607,27 +588,17 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
 #pragma unroll
     for (int i = 0; i < NLD; i++)
       roff[i] = (uint32_t)(min(RPW * li + RPI * i + lr, nrows - 1) * a.stride);
-    // DynamoRIO: one more load per tile, the previous chunk's last row (loader 0, lanes 0-15:
-    // 16 B each; every other lane repeats lane 0's address), for row 0's neighbour test.  Chunk
-    // 0 re-loads its own row 0 and ignores it (k_skip compares it across batches / shards).
-    const uint8_t *pbase = a.traces + (row0 ? row0 - 1 : 0) * a.stride +
-                           ((li == 0 && lane < SLOTS) ? lane * 16 : 0);
-    auto load_half = [&](u32x4 (&r)[NLD + NE], uint32_t t) {  // branch-free (see k_pass1s)
+    auto load_half = [&](u32x4 (&r)[NLD], uint32_t t) {  // branch-free (see k_pass1s)
       const uint32_t msk = t < ntiles ? ~0u : 0u;
 #pragma unroll
       for (int i = 0; i < NLD; i++) asm_load16(r[i], lbase + ((t * TW + roff[i]) & msk));
-      if (NE) asm_load16_cached(r[NLD + NE - 1], pbase + ((t * TW) & msk));
     };
-    auto store_half = [&](const u32x4 (&r)[NLD + NE], int b) {
+    auto store_half = [&](const u32x4 (&r)[NLD], int b) {
 #pragma unroll
       for (int i = 0; i < NLD; i++) {
         const int rr = RPW * li + RPI * i + lr;
         const u32x4 v = r[i];
         lds[b * TILE + rr * SLOTS + (ls ^ (rr & 15))] = make_uint4(v.x, v.y, v.z, v.w);
-      }
-      if (NE && li == 0 && lane < SLOTS) {
-        const u32x4 v = r[NLD + NE - 1];
-        ((uint4 *)&prv[b][0])[lane] = make_uint4(v.x, v.y, v.z, v.w);
       }
     };
     uint64_t h = (uint64_t)(kHashConst ^ a.map_size);
@@ -657,7 +628,7 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
       }
     };
     if (isLd) {  // the whole ring lives inside this wave-uniform branch
-      u32x4 R[D][NLD + NE];
+      u32x4 R[D][NLD];
 #pragma unroll
       for (int d = 0; d < D; d++) load_half(R[d], d);
       for (uint32_t g = 0; g < nsteps; g += D) {
@@ -667,7 +638,7 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
 #ifndef KBZ_XP_NOCHAIN
           if (isL && s >= 2 && s - 2 < ntiles) chain_tile(s - 2);
 #endif
-          vmcnt_wait_ring<(D - 1) * (NLD + NE)>(R[u]);
+          vmcnt_wait_ring<(D - 1) * NLD>(R[u]);
           store_half(R[u], s % 3);
           load_half(R[u], s + D);
           lds_barrier();
@@ -800,10 +771,8 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
     uint64_t *tfbase = a.tflags + (size_t)chunk * NC * a.nfw;
     auto finish_tile = [&](uint32_t t) {
       if (MODE == KBZ_MODE_DYNAMORIO) {
-        // group 0's first row is row 0: against the previous chunk's last row (chunk 0: 0, a
-        // placeholder k_skip does not use)
-        const uint64_t pl = grp > 0 ? bnd[t & 1][grp - 1][w]
-                                    : (chunk > 0 ? classify8(prv[t % 3][w]) : 0);
+        // group 0's first row is row 0: against 0, a placeholder k_skip does not use
+        const uint64_t pl = grp > 0 ? bnd[t & 1][grp - 1][w] : 0;
         const uint64_t bal = __ballot(((ftw ^ pl) & frel) != 0);
         nm |= ((uint64_t)((uint32_t)bal != 0) << r0a) |
               ((uint64_t)((uint32_t)(bal >> 32) != 0) << r0b);
@@ -864,25 +833,77 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
 // (shard_last[1], bit 0 = non-empty), bit 1 = "has a bad row j >= 1" and bit 2 = "has a
 // non-skipped row j >= 1": a shard with bit 2 and without bit 1 ends in a clean row (its last
 // row's chain of links starts at a row that was applied), whatever its row 0 is.
-__global__ void k_skip(const uint32_t *h32, const uint8_t *neq, uint32_t n, uint8_t *skip,
+// Row j's content against row j-1's on the examined bytes (classify_counts applied to both; with
+// ignore bytes only bytes whose ignore byte is 0), 16 B per thread per step: a block-wide OR.
+__device__ __forceinline__ int rows_differ(const uint8_t *x, const uint8_t *y, const uint8_t *ignore,
+                                           uint32_t map_size) {
+  int diff = 0;
+  for (uint32_t i = threadIdx.x * 16; i < map_size; i += blockDim.x * 16) {
+    const uint4 a = *(const uint4 *)(x + i), b = *(const uint4 *)(y + i);
+    const uint64_t a0 = classify8((uint64_t)a.x | ((uint64_t)a.y << 32));
+    const uint64_t a1 = classify8((uint64_t)a.z | ((uint64_t)a.w << 32));
+    const uint64_t b0 = classify8((uint64_t)b.x | ((uint64_t)b.y << 32));
+    const uint64_t b1 = classify8((uint64_t)b.z | ((uint64_t)b.w << 32));
+    uint64_t r0 = ~0ull, r1 = ~0ull;
+    if (ignore) {
+      const uint4 g = *(const uint4 *)(ignore + i);
+      r0 = ~nonzero_bytes8((uint64_t)g.x | ((uint64_t)g.y << 32));
+      r1 = ~nonzero_bytes8((uint64_t)g.z | ((uint64_t)g.w << 32));
+    }
+    diff |= (((a0 ^ b0) & r0) | ((a1 ^ b1) & r1)) != 0;
+  }
+  return __syncthreads_or(diff);
+}
+
+// k_skip (in kbz_shard_begin, rows j >= 1: they need no other shard) lists the chunks of bad
+// rows and queues those rows for k_chain.  Pass 1 compared every row with its predecessor
+// inside the chunk (neq); a chunk's row 0 has none there, so for j = 64c the extra blocks
+// compare the two rows themselves -- only when their hashes are equal (the only case the rule
+// looks at), which leaves the streaming pass without the previous chunk's row.  The shard's
+// last-hash pair (shard_last[1], bit 0 = non-empty) gets bit 1 = "has a bad row j >= 1" and
+// bit 2 = "has a non-skipped row j >= 1": a shard with bit 2 and without bit 1 ends in a clean
+// row (its last row's chain of links starts at a row that was applied), whatever its row 0 is.
+__global__ void k_skip(const uint32_t *h32, uint8_t *neq, uint32_t n, uint8_t *skip,
                        uint32_t *flags, uint32_t *fix_list, uint32_t *fix_cnt, uint32_t *bad_list,
-                       uint32_t *bad_cnt, uint32_t *shard_last) {
+                       uint32_t *bad_cnt, uint32_t *shard_last, const uint8_t *traces,
+                       size_t stride, const uint8_t *ignore, uint32_t map_size,
+                       uint32_t row_blocks) {
+  auto bad_row = [&](uint32_t j) {
+    const uint32_t c = j / kChunk;
+    if (atomicExch(&flags[c], 1u) == 0u) fix_list[atomicAdd(fix_cnt, 1u)] = c;
+    bad_list[atomicAdd(bad_cnt, 1u)] = j;
+  };
+  if (blockIdx.x >= row_blocks) {  // chunk start j = 64 c, c >= 1
+    const uint32_t j = (blockIdx.x - row_blocks + 1) * kChunk;
+    if (j >= n || h32[j] != h32[j - 1]) return;  // block-uniform
+    const uint8_t *x = traces + (size_t)j * stride;
+    const int diff = rows_differ(x, x - stride, ignore, map_size);
+    if (threadIdx.x == 0) {
+      neq[j] = diff != 0;  // exact now: k_chain's chain walks read it
+      if (diff) {
+        bad_row(j);
+        atomicOr(&shard_last[1], 2u);
+      }
+    }
+    return;
+  }
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   bool applied = false, bad = false;
   if (j >= 1 && j < n) {
     const bool sk = h32[j] == h32[j - 1];
     skip[j] = sk;
     applied = !sk;
-    if (sk && neq[j]) {
+    if (sk && (j % kChunk) && neq[j]) {
       bad = true;
-      const uint32_t c = j / kChunk;
-      if (atomicExch(&flags[c], 1u) == 0u) fix_list[atomicAdd(fix_cnt, 1u)] = c;
-      bad_list[atomicAdd(bad_cnt, 1u)] = j;
+      bad_row(j);
     }
   }
-  const uint64_t ap = __ballot(applied), bd = __ballot(bad);
-  if ((threadIdx.x & 63) == 0 && (ap || bd))
-    atomicOr(&shard_last[1], (bd ? 2u : 0u) | (ap ? 4u : 0u));
+  // one atomic per block at most (a flag word every wave hits serialises), skipped when the
+  // bits are already set
+  const int ap = __syncthreads_or(applied), bd = __syncthreads_or(bad);
+  const uint32_t want = (bd ? 2u : 0u) | (ap ? 4u : 0u);
+  if (threadIdx.x == 0 && (want & ~*(volatile uint32_t *)&shard_last[1]))
+    atomicOr(&shard_last[1], want);
 }
 
 // Predecessor of the shard's row 0 (kbz_shard_link): unknown, the context's saved row (the
@@ -933,24 +954,8 @@ __global__ __launch_bounds__(256) void k_chain(ChainArgs a) {
     const bool sk0 = a.h32[0] == hp;
     const bool known = a.pred_kind == PRED_SAVED ? *a.pred_ok != 0
                        : a.pred_kind == PRED_PAIR ? pair_clean(*a.pred_ok) : false;
-    int diff = 0;
-    if (sk0 && known) {  // row 0 against its predecessor, 16 B per thread per step
-      for (uint32_t i = threadIdx.x * 16; i < a.map_size; i += blockDim.x * 16) {
-        const uint4 x = *(const uint4 *)(a.row0 + i), y = *(const uint4 *)(a.prow + i);
-        const uint64_t x0 = classify8((uint64_t)x.x | ((uint64_t)x.y << 32));
-        const uint64_t x1 = classify8((uint64_t)x.z | ((uint64_t)x.w << 32));
-        const uint64_t y0 = classify8((uint64_t)y.x | ((uint64_t)y.y << 32));
-        const uint64_t y1 = classify8((uint64_t)y.z | ((uint64_t)y.w << 32));
-        uint64_t r0 = ~0ull, r1 = ~0ull;
-        if (a.ignore) {
-          const uint4 g = *(const uint4 *)(a.ignore + i);
-          r0 = ~nonzero_bytes8((uint64_t)g.x | ((uint64_t)g.y << 32));
-          r1 = ~nonzero_bytes8((uint64_t)g.z | ((uint64_t)g.w << 32));
-        }
-        diff |= (((x0 ^ y0) & r0) | ((x1 ^ y1) & r1)) != 0;
-      }
-    }
-    diff = __syncthreads_or(diff);
+    // row 0 against its predecessor (block-uniform condition)
+    const int diff = (sk0 && known) ? rows_differ(a.row0, a.prow, a.ignore, a.map_size) : 0;
     bad0 = sk0 && (!known || diff);
     if (threadIdx.x == 0) a.skip[0] = sk0;
   }
@@ -1077,9 +1082,32 @@ __device__ __forceinline__ uint32_t wave_excl_prefix(uint32_t v, uint32_t &total
   total = __shfl(x, 63);
   return x - v;
 }
+// A wave's claim items are staged in LDS and appended to the global list with ONE atomic per
+// flush (a global counter hit once per chunk by every wave serialises: 32k atomics on one
+// address cost ~0.3 ms on a fresh virgin map).
+constexpr int kWaveItems = 256;
+struct ItemStage {
+  uint64_t *buf;  // this wave's LDS staging area, kWaveItems entries
+  uint32_t n;     // wave-uniform fill
+};
+__device__ __forceinline__ void flush_items(ItemStage &st, uint64_t *items, uint32_t cap,
+                                            uint32_t *counters) {
+  if (!st.n) return;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's staged writes are done
+  uint32_t base = 0;
+  if ((threadIdx.x & 63) == 0) base = atomicAdd(&counters[0], st.n);
+  base = __shfl(base, 0);
+  for (uint32_t i = threadIdx.x & 63; i < st.n; i += 64) {
+    if (base + i < cap) items[base + i] = st.buf[i];
+    else atomicOr(&counters[1], 1u);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the area is reused
+  st.n = 0;
+}
 __device__ __forceinline__ void emit_items_wave(uint32_t chunk, int k, uint32_t col, uint4 nb,
-                                                uint4 vir, uint4 prev, uint64_t *items,
-                                                uint32_t cap, uint32_t *counters) {
+                                                uint4 vir, uint4 prev, ItemStage &st,
+                                                uint64_t *items, uint32_t cap,
+                                                uint32_t *counters) {
   const uint32_t w[4] = {nb.x, nb.y, nb.z, nb.w};
   const uint32_t vv[4] = {vir.x, vir.y, vir.z, vir.w};
   const uint32_t pv[4] = {prev.x, prev.y, prev.z, prev.w};
@@ -1088,9 +1116,14 @@ __device__ __forceinline__ void emit_items_wave(uint32_t chunk, int k, uint32_t 
   for (int i = 0; i < 4; i++) cnt += __popc(nonzero_bytes8(w[i]) & 0x80808080u);
   uint32_t total;
   const uint32_t off = wave_excl_prefix(cnt, total);
-  uint32_t base = 0;
-  if ((threadIdx.x & 63) == 63) base = atomicAdd(&counters[0], total);
-  base = __shfl(base, 63) + off;
+  if (st.n + total > kWaveItems) flush_items(st, items, cap, counters);
+  const bool staged = total <= kWaveItems;  // else (rare) straight to the global list
+  uint32_t base = st.n + off;
+  if (!staged) {
+    uint32_t g = 0;
+    if ((threadIdx.x & 63) == 63) g = atomicAdd(&counters[0], total);
+    base = __shfl(g, 63) + off;
+  }
 #pragma unroll
   for (int i = 0; i < 4; i++)
 #pragma unroll
@@ -1098,10 +1131,13 @@ __device__ __forceinline__ void emit_items_wave(uint32_t chunk, int k, uint32_t 
       const uint32_t x = (w[i] >> (8 * b)) & 0xff;
       if (!x) continue;
       const bool f2 = ((vv[i] >> (8 * b)) & 0xff) == 0xff && ((pv[i] >> (8 * b)) & 0xff) == 0;
-      if (base < cap) items[base] = pack_item(chunk, k, col + 4 * i + b, x, f2);
+      const uint64_t it = pack_item(chunk, k, col + 4 * i + b, x, f2);
+      if (staged) st.buf[base] = it;
+      else if (base < cap) items[base] = it;
       else atomicOr(&counters[1], 1u);
       base++;
     }
+  if (staged) st.n += total;
 }
 
 // Per (segment, 16-B column group): walk the segment's chunks in order with the running OR
@@ -1148,37 +1184,56 @@ __global__ __launch_bounds__(256) void k_scan(const uint8_t *chunk_or, const uin
   }
   const uint4 vr = live ? make_uint4(vir.x & rel.x, vir.y & rel.y, vir.z & rel.z, vir.w & rel.w)
                         : make_uint4(0, 0, 0, 0);
+  __shared__ uint64_t stage_buf[4][kWaveItems];  // 256 threads = 4 waves
+  ItemStage stg{stage_buf[threadIdx.x >> 6], 0u};
   const uint4 send = *(const uint4 *)((s + 1 < nseg) ? segprev + (size_t)(s + 1) * nclass * map_size + kc
                                                       : ltotal + kc);
   const uint32_t seg_new = (send.x & vr.x & ~prev.x) | (send.y & vr.y & ~prev.y) |
                            (send.z & vr.z & ~prev.z) | (send.w & vr.w & ~prev.w);
   if (!__ballot(seg_new != 0)) return;  // wave-uniform: nothing new in this segment
   const uint32_t c0 = s * seg_len, c1 = min(nchunks, c0 + seg_len);
-  // 8 chunks per batch, loads issued unconditionally (a chunk without traces of class k has a
-  // stale row: masked to 0 after the load) so each batch costs one memory round trip
-  for (uint32_t cb = c0; cb < c1; cb += 8) {
-    uint4 o[8];
-    bool st[8];
+  // Only chunks that hold traces of class k AND stored (or, DynamoRIO fix path, recomputed) one
+  // of this wave's 4 tiles can add bits here: an unstored tile held no still-virgin bit, so a
+  // skipped chunk changes neither the claims nor the running OR.  Lane l tests chunk cg + l;
+  // the wave walks the set bits of the ballot in order, 8 chunk loads per memory round trip.
+  const uint32_t t0 = (blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * 16 / kTileW;
+  for (uint32_t cg = c0; cg < c1; cg += 64) {
+    const uint32_t cl = cg + (threadIdx.x & 63);
+    bool any = false;
+    if (cl < c1 && ((chunk_cls[cl] >> k) & 1))
+      any = (listed && listed[cl]) ||
+            ((tflags[((size_t)cl * nclass + k) * nfw + (t0 >> 6)] >> (t0 & 63)) & 0xFull);
+    uint64_t mask = __ballot(any);
+    while (mask) {
+      uint32_t cs[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const uint32_t c = min(cb + u, c1 - 1);
-      o[u] = *(const uint4 *)(chunk_or + (size_t)c * nclass * map_size + kc);
-      // DynamoRIO fix path: a listed chunk's row was rewritten whole (unmasked) by k_total
-      st[u] = tile_stored(tflags, nfw, nclass, c, k, col) || (listed && listed[c]);
-    }
+      for (int u = 0; u < 8; u++) {
+        cs[u] = mask ? cg + (uint32_t)__builtin_ctzll(mask) : ~0u;
+        mask &= mask - 1;
+      }
+      uint4 o[8];
+      bool st[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const uint32_t c = cb + u;  // uniform across the block
-      if (c >= c1) break;
-      if (!((chunk_cls[c] >> k) & 1)) continue;
-      if (!st[u]) o[u] = make_uint4(0, 0, 0, 0);  // nothing still virgin in that tile
-      const uint4 nb = make_uint4(o[u].x & vr.x & ~prev.x, o[u].y & vr.y & ~prev.y,
-                                  o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
-      if (__ballot(nb.x | nb.y | nb.z | nb.w))  // wave-uniform: all lanes join the prefix
-        emit_items_wave(c, k, col, nb, vir, prev, items, cap, counters);
-      prev = or4(prev, o[u]);
+      for (int u = 0; u < 8; u++) {
+        const uint32_t c = cs[u] != ~0u ? cs[u] : cs[0];
+        o[u] = *(const uint4 *)(chunk_or + (size_t)c * nclass * map_size + kc);
+        // DynamoRIO fix path: a listed chunk's row was rewritten whole (unmasked) by k_total
+        st[u] = tile_stored(tflags, nfw, nclass, c, k, col) || (listed && listed[c]);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const uint32_t c = cs[u];  // uniform across the wave
+        if (c == ~0u) break;
+        if (!st[u]) o[u] = make_uint4(0, 0, 0, 0);  // nothing still virgin in that tile
+        const uint4 nb = make_uint4(o[u].x & vr.x & ~prev.x, o[u].y & vr.y & ~prev.y,
+                                    o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
+        if (__ballot(nb.x | nb.y | nb.z | nb.w))  // wave-uniform: all lanes join the prefix
+          emit_items_wave(c, k, col, nb, vir, prev, stg, items, cap, counters);
+        prev = or4(prev, o[u]);
+      }
     }
   }
+  flush_items(stg, items, cap, counters);
 }
 
 __global__ __launch_bounds__(256) void k_resolve(const uint8_t *traces, size_t stride, uint32_t n,
@@ -1228,10 +1283,12 @@ __global__ __launch_bounds__(256) void k_resolve(const uint8_t *traces, size_t s
 // last-hash pair.
 __global__ void k_pack(uint32_t *hnb32, const uint32_t *h32, uint32_t n, uint8_t *hnb_out,
                        uint32_t *h32_out, uint32_t *counters, uint32_t *flags, uint32_t nchunks,
-                       uint32_t *shard_last) {
+                       uint32_t *shard_last, uint32_t *err_out) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j < nchunks && flags) flags[j] = 0;
   if (j == 0) {
+    err_out[0] = counters[1];  // the sticky error flags, readable without a copy (host-mapped)
+    err_out[1] = counters[2];
     counters[8] = counters[0];   // kbz_ctx_stats: claim items, recomputed chunks, bad rows
     counters[9] = counters[3];
     counters[10] = counters[4];
@@ -1505,6 +1562,11 @@ struct kbz_ctx {
     uint8_t *d_hnb = nullptr, *h_hnb = nullptr;
     uint32_t *d_h32 = nullptr, *h_h32 = nullptr;
     uint64_t *d_x64 = nullptr, *h_x64 = nullptr;
+    // device views of the pinned rows / outcomes / results (zero-copy small batches)
+    uint8_t *m_rows = nullptr, *m_hnb = nullptr;
+    int8_t *m_oc = nullptr;
+    uint32_t *m_h32 = nullptr;
+    uint64_t *m_x64 = nullptr;
     size_t n = 0;
     bool pending = false;
     uint8_t *hnb_out = nullptr;
@@ -1513,6 +1575,7 @@ struct kbz_ctx {
   } ring[2];
   int ring_next = 0;        // slot the next kbz_ring_acquire returns
   int ring_acquired = -1;   // slot handed out and not yet submitted
+  uint32_t *h_err = nullptr, *d_err = nullptr;  // host-mapped copy of counters[1..2] (k_pack)
   // kbz_ctx_time_pass1: HIP events around every pass-1 launch (on its stream)
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pass1;
@@ -1580,6 +1643,7 @@ void free_ctx(kbz_ctx *c) {
     (void)hipEventDestroy(e.first);
     (void)hipEventDestroy(e.second);
   }
+  if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->work_stream) (void)hipStreamDestroy(c->work_stream);
   delete c;
@@ -1726,6 +1790,13 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
     g_err = e;
     return nullptr;
   }
+  if (hipHostMalloc((void **)&c->h_err, 2 * sizeof(uint32_t), hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&c->d_err, c->h_err, 0) != hipSuccess) {
+    fail("pinned error words");
+    free_ctx(c);
+    return nullptr;
+  }
+  c->h_err[0] = c->h_err[1] = 0;
   (void)hipMemset(c->V[0], 0xff, 3 * M);
   (void)hipMemset(c->last, 0, 2 * sizeof(uint32_t));
   (void)hipMemset(c->counters, 0, 16 * sizeof(uint32_t));
@@ -1886,9 +1957,11 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
   if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, s)) return -1;
   if (ev) HIP_TRY(hipEventRecord(c->ev_pass1[c->ev_used_n - 1].second, s));
   if (c->mode == KBZ_MODE_DYNAMORIO) {  // the skip rule for rows j >= 1 needs no other shard
-    hipLaunchKernelGGL(k_skip, dim3(cdiv(n, 256)), dim3(256), 0, s, c->cur_h32, c->neq,
-                       (uint32_t)n, c->skip, c->flags, c->fix_list, c->counters + 3, c->bad_list,
-                       c->counters + 4, c->shard_last);
+    const unsigned row_blocks = cdiv(n, 256);
+    hipLaunchKernelGGL(k_skip, dim3(row_blocks + c->cur_chunks - 1), dim3(256), 0, s, c->cur_h32,
+                       c->neq, (uint32_t)n, c->skip, c->flags, c->fix_list, c->counters + 3,
+                       c->bad_list, c->counters + 4, c->shard_last, traces, stride, c->ignore,
+                       (uint32_t)c->M, row_blocks);
     HIP_TRY(hipGetLastError());
   }
   c->stage = 1;
@@ -2044,7 +2117,7 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
                        (uint32_t)c->cur_n, hnb_out ? hnb_out : (uint8_t *)nullptr,
                        (c->cur_h32_out && c->cur_h32_out != c->cur_h32) ? c->cur_h32_out : nullptr,
                        c->counters, c->mode == KBZ_MODE_DYNAMORIO ? c->flags : nullptr,
-                       c->cur_chunks, c->shard_last);
+                       c->cur_chunks, c->shard_last, c->d_err);
     HIP_TRY(hipGetLastError());
   } else {
     // empty shard: k_skip may still have written the fix count / shard pair; re-arm them
@@ -2112,8 +2185,8 @@ int ensure_streaming(kbz_ctx *c) {
   HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&c->work_stream, hipStreamNonBlocking));
   for (int i = 0; i < 2; i++) {
-    HIP_TRY(hipHostMalloc((void **)&c->pin[i], rows * c->M, hipHostMallocDefault));
-    HIP_TRY(hipHostMalloc((void **)&c->pin_oc[i], rows, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void **)&c->pin[i], rows * c->M, hipHostMallocMapped));
+    HIP_TRY(hipHostMalloc((void **)&c->pin_oc[i], rows, hipHostMallocMapped));
     HIP_TRY(hipMalloc((void **)&c->dslot[i], rows * c->M));
     HIP_TRY(hipMalloc((void **)&c->dslot_oc[i], rows));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_copied[i], hipEventDisableTiming));
@@ -2196,14 +2269,20 @@ namespace {
 int ensure_ring(kbz_ctx *c) {
   if (ensure_streaming(c)) return -1;
   const size_t R = c->slot_rows;
-  for (auto &r : c->ring) {
+  for (int i = 0; i < 2; i++) {
+    auto &r = c->ring[i];
     if (r.d_hnb) continue;
     HIP_TRY(hipMalloc((void **)&r.d_hnb, R));
     HIP_TRY(hipMalloc((void **)&r.d_h32, R * 4));
     HIP_TRY(hipMalloc((void **)&r.d_x64, R * 8));
-    HIP_TRY(hipHostMalloc((void **)&r.h_hnb, R, hipHostMallocDefault));
-    HIP_TRY(hipHostMalloc((void **)&r.h_h32, R * 4, hipHostMallocDefault));
-    HIP_TRY(hipHostMalloc((void **)&r.h_x64, R * 8, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void **)&r.h_hnb, R, hipHostMallocMapped));
+    HIP_TRY(hipHostMalloc((void **)&r.h_h32, R * 4, hipHostMallocMapped));
+    HIP_TRY(hipHostMalloc((void **)&r.h_x64, R * 8, hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void **)&r.m_rows, c->pin[i], 0));
+    HIP_TRY(hipHostGetDevicePointer((void **)&r.m_oc, c->pin_oc[i], 0));
+    HIP_TRY(hipHostGetDevicePointer((void **)&r.m_hnb, r.h_hnb, 0));
+    HIP_TRY(hipHostGetDevicePointer((void **)&r.m_h32, r.h_h32, 0));
+    HIP_TRY(hipHostGetDevicePointer((void **)&r.m_x64, r.h_x64, 0));
   }
   return 0;
 }
@@ -2214,6 +2293,15 @@ void ring_deliver(kbz_ctx::RingSlot &r) {
   if (r.h32_out) memcpy(r.h32_out, r.h_h32, r.n * 4);
   if (r.x64_out) memcpy(r.x64_out, r.h_x64, r.n * 8);
   r.pending = false;
+}
+// The sticky device error flags, as k_pack last copied them into host-mapped memory: reported
+// (and cleared) without a device round trip.
+int ring_errors(kbz_ctx *c) {
+  if (!c->h_err[0] && !c->h_err[1]) return 0;
+  const bool ovf = c->h_err[0] != 0;
+  HIP_TRY(hipMemset(c->counters + 1, 0, 2 * sizeof(uint32_t)));
+  c->h_err[0] = c->h_err[1] = 0;
+  return fail(ovf ? "claim list overflow" : "inconsistent claim (internal error)");
 }
 }  // namespace
 
@@ -2229,8 +2317,13 @@ int kbz_ring_acquire(kbz_ctx_t *c, uint8_t **rows, int8_t **outcome, size_t *cap
   *rows = c->pin[sl];
   if (outcome) *outcome = c->pin_oc[sl];
   if (cap) *cap = c->slot_rows;
-  return 0;
+  return ring_errors(c);
 }
+
+// Batches of at most one chunk are triaged straight from the pinned slot and write their
+// results straight into pinned memory (the kernels read / write host memory over PCIe): no
+// DMA transfers on the latency path of a per-exec flush.
+constexpr size_t kZeroCopyRows = 64;
 
 int kbz_ring_submit(kbz_ctx_t *c, size_t n, int have_outcome, uint8_t *hnb_out,
                     uint32_t *h32_out, uint64_t *x64_out, int want) {
@@ -2241,23 +2334,31 @@ int kbz_ring_submit(kbz_ctx_t *c, size_t n, int have_outcome, uint8_t *hnb_out,
   DevGuard g(c->device);
   auto &r = c->ring[sl];
   const size_t M = c->M;
-  HIP_TRY(hipMemcpyAsync(c->dslot[sl], c->pin[sl], n * M, hipMemcpyHostToDevice, c->copy_stream));
-  if (have_outcome)
-    HIP_TRY(hipMemcpyAsync(c->dslot_oc[sl], c->pin_oc[sl], n, hipMemcpyHostToDevice,
-                           c->copy_stream));
-  HIP_TRY(hipEventRecord(c->ev_copied[sl], c->copy_stream));
-  HIP_TRY(hipStreamWaitEvent(c->work_stream, c->ev_copied[sl], 0));
   const bool x64 = (want & KBZ_WANT_X64) && x64_out;
-  if (kbz_triage_batch_device(c, c->dslot[sl], n, M, have_outcome ? c->dslot_oc[sl] : nullptr,
-                              r.d_hnb, h32_out ? r.d_h32 : nullptr, x64 ? r.d_x64 : nullptr,
-                              want, c->work_stream))
-    return -1;
-  if (n) {
-    HIP_TRY(hipMemcpyAsync(r.h_hnb, r.d_hnb, n, hipMemcpyDeviceToHost, c->work_stream));
-    if (h32_out)
-      HIP_TRY(hipMemcpyAsync(r.h_h32, r.d_h32, n * 4, hipMemcpyDeviceToHost, c->work_stream));
-    if (x64)
-      HIP_TRY(hipMemcpyAsync(r.h_x64, r.d_x64, n * 8, hipMemcpyDeviceToHost, c->work_stream));
+  if (n <= kZeroCopyRows) {
+    if (kbz_triage_batch_device(c, r.m_rows, n, M, have_outcome ? r.m_oc : nullptr, r.m_hnb,
+                                h32_out ? r.m_h32 : nullptr, x64 ? r.m_x64 : nullptr, want,
+                                c->work_stream))
+      return -1;
+  } else {
+    HIP_TRY(hipMemcpyAsync(c->dslot[sl], c->pin[sl], n * M, hipMemcpyHostToDevice,
+                           c->copy_stream));
+    if (have_outcome)
+      HIP_TRY(hipMemcpyAsync(c->dslot_oc[sl], c->pin_oc[sl], n, hipMemcpyHostToDevice,
+                             c->copy_stream));
+    HIP_TRY(hipEventRecord(c->ev_copied[sl], c->copy_stream));
+    HIP_TRY(hipStreamWaitEvent(c->work_stream, c->ev_copied[sl], 0));
+    if (kbz_triage_batch_device(c, c->dslot[sl], n, M, have_outcome ? c->dslot_oc[sl] : nullptr,
+                                r.d_hnb, h32_out ? r.d_h32 : nullptr, x64 ? r.d_x64 : nullptr,
+                                want, c->work_stream))
+      return -1;
+    if (n) {
+      HIP_TRY(hipMemcpyAsync(r.h_hnb, r.d_hnb, n, hipMemcpyDeviceToHost, c->work_stream));
+      if (h32_out)
+        HIP_TRY(hipMemcpyAsync(r.h_h32, r.d_h32, n * 4, hipMemcpyDeviceToHost, c->work_stream));
+      if (x64)
+        HIP_TRY(hipMemcpyAsync(r.h_x64, r.d_x64, n * 8, hipMemcpyDeviceToHost, c->work_stream));
+    }
   }
   HIP_TRY(hipEventRecord(c->ev_used[sl], c->work_stream));
   r.n = n;
@@ -2276,7 +2377,7 @@ int kbz_ring_flush(kbz_ctx_t *c) {
   DevGuard g(c->device);
   HIP_TRY(hipStreamSynchronize(c->work_stream));
   for (auto &r : c->ring) ring_deliver(r);
-  return kbz_sync(c, c->work_stream);
+  return ring_errors(c);
 }
 
 // ---- merger -----------------------------------------------------------------------------------

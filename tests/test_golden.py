@@ -194,3 +194,76 @@ def test_picker_gpu(gpu):
     np.testing.assert_array_equal(g_ign.cpu().numpy(), ign)
     np.testing.assert_array_equal(g_pc.cpu().numpy().view(np.uint32), pc)
     assert int(g_tot.item()) == tot
+
+
+# ---- BASELINE config 1: real afl-gcc traces of corpus/afl_test (tests/golden/make_config1.py) --
+
+C1_SEQS = ("aaaa", "abc")
+C1_MODES = (("afl", oracle.MODE_AFL), ("dynamorio", oracle.MODE_DYNAMORIO))
+
+
+def c1_traces(f, tag):
+    n = int(f[f"{tag}_n"])
+    return dense(n, 65536, f[f"{tag}_tj"], f[f"{tag}_ti"], f[f"{tag}_tv"]), f[f"{tag}_outcome"]
+
+
+def test_config1_fixture_sanity(oracle_lib):
+    """The captured runs behave as the reference's smoke test expects (sanity, not parity: the
+    bit_flip mutator is external): tests/smoke_test.sh:139-145 wants 2 new paths in 10 execs
+    from "AAAA", :172-175 a crash from "ABC@"."""
+    f = load("config1.npz")
+    assert int(f["smoke_new_paths"]) == 2
+    assert (f["abc_outcome"] == oracle.FUZZ_CRASH).sum() >= 1
+    assert (f["aaaa_outcome"] == oracle.FUZZ_NONE).all()
+
+
+@pytest.mark.parametrize("tag", C1_SEQS)
+@pytest.mark.parametrize("name,mode", C1_MODES)
+def test_config1_oracle(oracle_lib, tag, name, mode):
+    f = load("config1.npz")
+    t, oc = c1_traces(f, tag)
+    r = oracle.triage_batch(mode, t, oc, want=oracle.WANT_H32 | oracle.WANT_X64)
+    np.testing.assert_array_equal(r["hnb"], f[f"{tag}_{name}_hnb"])
+    np.testing.assert_array_equal(r["h32"], f[f"{tag}_{name}_h32"])
+    np.testing.assert_array_equal(r["x64"], f[f"{tag}_{name}_x64"])
+    np.testing.assert_array_equal(r["virgin"], virgin(65536, f[f"{tag}_{name}_vmap"],
+                                                      f[f"{tag}_{name}_vidx"],
+                                                      f[f"{tag}_{name}_vval"]))
+    if mode == oracle.MODE_DYNAMORIO:
+        assert r["last_hash"] == int(f[f"{tag}_{name}_last"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pass1", ["narrow", "wide"])
+@pytest.mark.parametrize("split", [0, 7, 64])
+@pytest.mark.parametrize("tag", C1_SEQS)
+@pytest.mark.parametrize("name,mode", C1_MODES)
+def test_config1_gpu(gpu, tag, name, mode, split, pass1):
+    """The real traces through libkbz_hip.so: one batch (split 0) or consecutive batches of
+    `split` execs with the state carried, against the reference's own per-exec results."""
+    import torch
+
+    from killerbeez_amd.triage import WANT_H32, WANT_X64, TriageContext
+
+    f = load("config1.npz")
+    t, oc = c1_traces(f, tag)
+    n = t.shape[0]
+    step = split or n
+    hnb, h32, x64 = [], [], []
+    with TriageContext(65536, mode, step, pass1=pass1) as ctx:
+        for lo in range(0, n, step):
+            out = ctx.triage(torch.from_numpy(t[lo:lo + step]).cuda(),
+                             torch.from_numpy(oc[lo:lo + step]).cuda(), WANT_H32 | WANT_X64)
+            torch.cuda.synchronize()
+            ctx.sync()
+            hnb.append(out["hnb"].cpu().numpy())
+            h32.append(out["h32"].cpu().numpy().view(np.uint32))
+            x64.append(out["x64"].cpu().numpy().view(np.uint64))
+        np.testing.assert_array_equal(np.concatenate(hnb), f[f"{tag}_{name}_hnb"])
+        np.testing.assert_array_equal(np.concatenate(h32), f[f"{tag}_{name}_h32"])
+        np.testing.assert_array_equal(np.concatenate(x64), f[f"{tag}_{name}_x64"])
+        np.testing.assert_array_equal(ctx.get_virgin(), virgin(65536, f[f"{tag}_{name}_vmap"],
+                                                               f[f"{tag}_{name}_vidx"],
+                                                               f[f"{tag}_{name}_vval"]))
+        if mode == oracle.MODE_DYNAMORIO:
+            assert ctx.last_hash == int(f[f"{tag}_{name}_last"])

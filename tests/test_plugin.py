@@ -92,9 +92,11 @@ def test_no_cpu_fallback():
     p = P.Plugin("afl_gpu", f'{{"map_size": {M}}}')
     t = np.zeros(M, np.uint8)
     t[5] = 1
-    assert p.record(t, P.FUZZ_NONE) == 0
-    assert p.is_new_path() == -1  # the triage needs the GPU: it fails, nothing computes on CPU
-    assert P.last_error()
+    # the exec's trace goes straight into a pinned GPU ring slot: without a GPU, recording
+    # fails and nothing computes on the CPU
+    assert p.record(t, P.FUZZ_NONE) == -1
+    assert "GPU" in P.last_error()
+    assert p.is_new_path() == -1
     q = P.Plugin("afl_gpu", f'{{"map_size": {M}}}')
     with pytest.raises(RuntimeError, match="merge"):
         p.merge(q)
@@ -188,3 +190,25 @@ def test_state_load_continue_and_merge(gpu, name, mode):
         np.testing.assert_array_equal(P.state_maps(mm.get_state(), M)[k], va[k] & vb[k] & vc[k])
     if name == "dynamorio_gpu":
         assert P.state_maps(mm.get_state(), M)["last_shm_hash"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,mode", MODES)
+def test_config1_real_traces_per_exec(gpu, name, mode):
+    """BASELINE config 1 through the plugin as fuzzer/main.c:374-385 drives it (one exec, then
+    is_new_path): the real afl-gcc traces of corpus/afl_test (tests/golden/config1.npz), whose
+    expected results come from the reference's own code; "ABC@" reaches the crash."""
+    f = np.load(os.path.join(os.path.dirname(__file__), "golden", "config1.npz"))
+    key = "afl" if name == "afl_gpu" else "dynamorio"
+    for tag in ("abc", "aaaa"):
+        n = int(f[f"{tag}_n"])
+        t = np.zeros((n, 65536), np.uint8)
+        t[f[f"{tag}_tj"], f[f"{tag}_ti"]] = f[f"{tag}_tv"]
+        oc = f[f"{tag}_outcome"]
+        exp = f[f"{tag}_{key}_hnb"]
+        p = P.Plugin(name, '{"map_size": 65536, "max_batch": 64}')
+        for j in range(min(n, 300)):
+            assert p.record(t[j], int(oc[j])) == j
+            assert p.is_new_path() == int(exp[j] != 0), (tag, j)
+            assert p.get_fuzz_result() == oc[j]
+        p.close()
