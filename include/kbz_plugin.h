@@ -61,12 +61,14 @@ extern "C" {
 #define KBZ_PLUGIN_FUZZ_CRASH 2
 #define KBZ_PLUGIN_FUZZ_ERROR (-1)
 
-/* instrumentation/instrumentation.h:17-37 (edge list of the optional get_edges, x64 layout) */
+/* instrumentation/instrumentation.h:17-37 (edge list of the optional get_edges).  The
+ * reference selects 64-bit fields with MSVC's _M_X64 only, so its Linux build uses 32-bit ones;
+ * this is that layout (tests/native/abi_layout.c checks it against the reference header). */
 typedef struct kbz_instrumentation_edge {
-  uint64_t from, to;
+  uint32_t from, to;
 } kbz_instrumentation_edge_t;
 typedef struct kbz_instrumentation_edges {
-  uint64_t num_edges;
+  uint32_t num_edges;
   kbz_instrumentation_edge_t edges[1];
 } kbz_instrumentation_edges_t;
 

@@ -212,6 +212,12 @@ int kbz_triage_modules_device(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *t
                               size_t stride, const size_t *module_offsets, const int8_t *outcome,
                               uint8_t *hnb_out, uint8_t *any_out, void *stream);
 
+/* Host-memory variant (traces, module_offsets, outcome, hnb_out [k*n], any_out [n] all host
+ * memory).  Synchronous. */
+int kbz_triage_modules_host(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *traces, size_t n,
+                            size_t stride, const size_t *module_offsets, const int8_t *outcome,
+                            uint8_t *hnb_out, uint8_t *any_out);
+
 /* ---- picker: ignore bytes from repeated runs ------------------------------------------------ */
 /* The picker's diff loop (picker/main.c:240-262) for one module: runs = device
  * [files][iters][size] bytes, the instrumentation data of iteration `it` of input file `f`
@@ -251,6 +257,10 @@ const char *kbz_set_last_error(void);
  * inserted nor new); is_new_out: device uint8[n] (1 = new, inserted).  Stream-ordered. */
 int kbz_set_insert_device(kbz_set_t *set, const uint64_t *keys, const uint8_t *mask, size_t n,
                           uint8_t *is_new_out, void *stream);
+/* Host variant: keys host uint64[2*n] inserted in order (e.g. a state's key list being loaded:
+ * linux_ipt_set_state :1066-1075 adds each key not yet present); is_new_out host or NULL.
+ * Synchronous. */
+int kbz_set_insert_host(kbz_set_t *set, const uint64_t *keys, size_t n, uint8_t *is_new_out);
 /* Number of keys in the set; -1 if the capacity was exceeded (keys dropped).  Synchronous. */
 int kbz_set_size(kbz_set_t *set, size_t *out);
 /* The first min(cap, size) keys in insertion order into host uint64[2*cap]; *n_out = size.
@@ -261,6 +271,42 @@ int kbz_set_keys(kbz_set_t *set, uint64_t *host_out, size_t cap, size_t *n_out);
  * of second absent from first, in second's insertion order.  Neither input is changed.  Runs on
  * the device, ordered on `stream`; NULL on failure (kbz_set_last_error). */
 kbz_set_t *kbz_set_merge(kbz_set_t *first, kbz_set_t *second, void *stream);
+
+/* ---- Intel-PT path keys (linux_ipt_instrumentation.c analyze_ipt :212-425) ------------------- */
+/* The reference hashes every exec's IPT packets into two streaming XXH64s while parsing them:
+ * TNT bits via add_tnt_to_hash (:132-156), TIP addresses via add_tip_to_hash (:163-189),
+ * finish_tnt_hash (:115-124) at the end, and looks the digest pair {tip, tnt} up in its set
+ * (:409-424).  Here the host-side parser (it stays on the CPU) feeds a batch of execs, each
+ * call the counterpart of the reference function named; the digests of the whole batch are
+ * computed on the GPU, and novelty is the unique set (kbz_set_*: insert-if-absent, insertion
+ * order = the reference's uthash set; its state dump/load is kbz_set_keys / kbz_set_insert_host,
+ * linux_ipt_merge is kbz_set_merge). */
+typedef struct kbz_ipt_batch kbz_ipt_batch_t;
+kbz_ipt_batch_t *kbz_ipt_batch_create(void);
+void kbz_ipt_batch_destroy(kbz_ipt_batch_t *batch);
+const char *kbz_ipt_last_error(void);
+/* add_tip_to_hash's ASLR normalisation (:169-185): a TIP inside coverage library i (starts[i] <=
+ * tip < ends[i]) becomes (tip - starts[i]) | library_hashes[i] << 32; without libraries, one
+ * inside [target_start, target_end) becomes tip - target_start; others are kept. */
+int kbz_ipt_set_ranges(kbz_ipt_batch_t *batch, size_t n_libraries, const uint64_t *starts,
+                       const uint64_t *ends, const uint32_t *library_hashes,
+                       uint64_t target_start, uint64_t target_end);
+/* add_tnt_to_hash: num_bits TNT bits of one packet (tnt_bits[i / 8] bit i % 8). */
+int kbz_ipt_add_tnt(kbz_ipt_batch_t *batch, const uint8_t *tnt_bits, int num_bits);
+/* add_tip_to_hash: the IP of a TIP packet. */
+int kbz_ipt_add_tip(kbz_ipt_batch_t *batch, uint64_t tip);
+/* finish_tnt_hash: the current exec is complete (the next add starts a new one). */
+int kbz_ipt_end_exec(kbz_ipt_batch_t *batch);
+size_t kbz_ipt_execs(kbz_ipt_batch_t *batch);
+/* keys_out: device uint64[2*n], {tip digest, tnt digest} per completed exec (the
+ * ipt_hashtable_key of linux_ipt_instrumentation.h:19-22).  Uploads the batch, queues the
+ * hashes on `stream` and empties the batch. */
+int kbz_ipt_hash_device(kbz_ipt_batch_t *batch, uint64_t *keys_out, void *stream);
+/* The whole novelty step for the batch: hashes, then insert into `set` in exec order;
+ * keys_out (host uint64[2*n] or NULL) and is_new_out (host uint8[n] or NULL: 1 = the exec's path
+ * was new, linux_ipt_is_new_path's result).  Synchronous; empties the batch. */
+int kbz_ipt_triage(kbz_ipt_batch_t *batch, kbz_set_t *set, uint64_t *keys_out,
+                   uint8_t *is_new_out);
 
 #ifdef __cplusplus
 }

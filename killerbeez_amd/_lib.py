@@ -47,6 +47,7 @@ SIGNATURES = [
     ("kbz_merge_and_device", _i, [_vp, _vp, _sz, _sz, _vp]),
     ("kbz_merge_and_host", _i, [_vp, _vp, _sz, _sz]),
     ("kbz_triage_modules_device", _i, [_vp, _sz, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp]),
+    ("kbz_triage_modules_host", _i, [_vp, _sz, _vp, _sz, _sz, _vp, _vp, _vp, _vp]),
     ("kbz_picker_ignore_device", _i, [_vp, _sz, _sz, _sz, _vp, _vp, _vp, _vp]),
     ("kbz_hash32_device", _i, [_vp, _sz, _sz, _sz, _u32, _vp, _vp]),
     ("kbz_xxh64_device", _i, [_vp, _sz, _sz, _sz, _u64, _vp, _vp]),
@@ -58,6 +59,17 @@ SIGNATURES = [
     ("kbz_set_size", _i, [_vp, C.POINTER(_sz)]),
     ("kbz_set_keys", _i, [_vp, _vp, _sz, C.POINTER(_sz)]),
     ("kbz_set_merge", _vp, [_vp, _vp, _vp]),
+    ("kbz_set_insert_host", _i, [_vp, _vp, _sz, _vp]),
+    ("kbz_ipt_batch_create", _vp, []),
+    ("kbz_ipt_batch_destroy", None, [_vp]),
+    ("kbz_ipt_last_error", C.c_char_p, []),
+    ("kbz_ipt_set_ranges", _i, [_vp, _sz, _vp, _vp, _vp, _u64, _u64]),
+    ("kbz_ipt_add_tnt", _i, [_vp, _vp, _i]),
+    ("kbz_ipt_add_tip", _i, [_vp, _u64]),
+    ("kbz_ipt_end_exec", _i, [_vp]),
+    ("kbz_ipt_execs", _sz, [_vp]),
+    ("kbz_ipt_hash_device", _i, [_vp, _vp, _vp]),
+    ("kbz_ipt_triage", _i, [_vp, _vp, _vp, _vp]),
 ]
 
 

@@ -17,7 +17,8 @@ HIP_LIB = os.path.join(PKG, "libkbz_hip.so")
 PLUGIN_LIB = os.path.join(PKG, "libkbz_plugin.so")
 ARCH = os.environ.get("KBZ_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = [os.path.join(CSRC, "kbz_triage.hip"), os.path.join(CSRC, "kbz_set.hip")]
+HIP_SOURCES = [os.path.join(CSRC, "kbz_triage.hip"), os.path.join(CSRC, "kbz_set.hip"),
+               os.path.join(CSRC, "kbz_ipt.hip")]
 HIP_HEADERS = [os.path.join(CSRC, "kbz_device.h"), os.path.join(INC, "kbz_triage.h")]
 PLUGIN_SOURCES = [os.path.join(CSRC, "kbz_plugin.c")]
 PLUGIN_HEADERS = [os.path.join(INC, "kbz_plugin.h"), os.path.join(INC, "kbz_triage.h")]

@@ -13,14 +13,20 @@
  *   create/set_state      afl_create :23-35, afl_set_state :95-109 (3 maps), dynamorio_set_state
  *                         :1311-1372 (virgin_bits + last_shm_hash); fresh maps are all-0xff
  *                         (setup_shm afl_instrumentation.c:555-559)
- *   get_state             afl_get_state :62-79, dynamorio_get_state :1239-1281 (key names)
+ *   get_state             afl_get_state :62-79, dynamorio_get_state :1239-1281 (key names;
+ *                         per_module_coverage: a "modules" array of {name, virgin_bits,
+ *                         last_shm_hash, last_path_was_new})
  *   merge                 afl_merge :123-140 (AND of the 3 maps, everything else fresh),
  *                         dynamorio_merge :1180-1231 (AND of virgin_bits, last hash 0)
  *   is_new_path           afl_is_new_path :189-198 (last_is_new_path ? 1 : 0; -1 before the
  *                         first exec), dynamorio has_new_coverage :1465-1467 (hnb != 0)
  *   get_fuzz_result       afl_get_fuzz_result :208-216 (the recorded FUZZ_* of the last exec)
  *   ignore_bytes_file     load_ignore_bytes dynamorio_instrumentation.c:788-801 (exactly
- *                         map_size bytes)
+ *                         map_size bytes); ignore_bytes_dir (per module: <dir>/<name>.dat, :802-814)
+ *   per_module_coverage   dynamorio_instrumentation.c:1048-1063 options, has_new_coverage_per_
+ *                         module :1477-1493 (own virgin map / ignore bytes / last hash per module,
+ *                         the exec is new if any module is), dynamorio_merge :1180-1231 (modules
+ *                         matched by name)
  */
 #define _POSIX_C_SOURCE 200809L /* strdup under -std=c11 */
 #include "kbz_plugin.h"
@@ -61,6 +67,21 @@ typedef struct kbz_plugin {
   long r_base;
   long last_ticket;        /* -1 until the first record */
   int last_fuzz_result;
+  int last_path_was_new;   /* has_new_coverage result of the last triaged exec (DR state key) */
+  /* dynamorio_gpu per_module_coverage (dynamorio_instrumentation.c:1048-1063): nmod module maps
+   * per exec, each with its own context (virgin map, ignore bytes, last hash).  The queue is a
+   * host buffer of max_batch rows of nmod*map_size bytes (module m at offset m*map_size). */
+  int per_module;
+  size_t nmod;
+  char **mod_names;
+  kbz_ctx_t **mctx;
+  uint8_t *mvirgin;        /* [nmod][map_size] host mirror */
+  uint32_t *mlast;         /* [nmod] last_shm_hash */
+  uint8_t *mnew;           /* [nmod] last_path_was_new */
+  uint8_t **mignore;       /* [nmod] ignore bytes or NULL */
+  uint8_t *mq;             /* queued execs, max_batch rows */
+  int8_t *mq_outcome;
+  uint8_t *r_mhnb;         /* [nmod][max_batch] per-module results of the last window */
 } kbz_plugin_t;
 
 static size_t nmaps(const kbz_plugin_t *p) { return p->mode == KBZ_MODE_DYNAMORIO ? 1 : 3; }
@@ -106,6 +127,77 @@ static char *json_str(const char *json, const char *key) {
   return s;
 }
 
+/* The raw text of a JSON array value ("[...]") -> its top-level elements as malloc'd strings
+ * (quotes kept for strings, braces for objects); NULL + *n = 0 when the key is absent. */
+static char **json_array(const char *json, const char *key, size_t *n, int *bad) {
+  *n = 0;
+  *bad = 0;
+  const char *v = json ? json_value(json, key) : NULL;
+  if (!v) return NULL;
+  if (*v != '[') {
+    *bad = 1;
+    return NULL;
+  }
+  char **items = NULL;
+  const char *q = v + 1;
+  for (;;) {
+    while (*q == ' ' || *q == '\t' || *q == '\n' || *q == '\r' || *q == ',') q++;
+    if (*q == ']') return items;
+    if (!*q) break;
+    const char *b = q;
+    int depth = 0, in_str = 0;
+    for (; *q; q++) {
+      if (in_str) {
+        if (*q == '\\' && q[1]) q++;
+        else if (*q == '"') in_str = 0;
+        if (!in_str && !depth) {
+          q++;
+          break;
+        }
+        continue;
+      }
+      if (*q == '"') in_str = 1;
+      else if (*q == '{' || *q == '[') depth++;
+      else if (*q == '}' || *q == ']') {
+        if (!depth) break;
+        if (!--depth) {
+          q++;
+          break;
+        }
+      } else if (*q == ',' && !depth) break;
+    }
+    char **grown = (char **)realloc(items, (*n + 1) * sizeof(char *));
+    if (!grown) break;
+    items = grown;
+    items[*n] = strndup(b, (size_t)(q - b));
+    if (!items[*n]) break;
+    (*n)++;
+  }
+  *bad = 1;
+  for (size_t i = 0; i < *n; i++) free(items[i]);
+  free(items);
+  *n = 0;
+  return NULL;
+}
+static void free_strings(char **v, size_t n) {
+  if (!v) return;
+  for (size_t i = 0; i < n; i++) free(v[i]);
+  free(v);
+}
+/* a JSON string element ("...") -> malloc'd unescaped text */
+static char *json_unquote(const char *s) {
+  if (!s || *s != '"') return NULL;
+  char *o = (char *)malloc(strlen(s));
+  if (!o) return NULL;
+  size_t n = 0;
+  for (s++; *s && *s != '"'; s++) {
+    if (*s == '\\' && s[1]) s++;
+    o[n++] = *s;
+  }
+  o[n] = 0;
+  return o;
+}
+
 static int hexval(char c) {
   if (c >= '0' && c <= '9') return c - '0';
   if (c >= 'a' && c <= 'f') return c - 'a' + 10;
@@ -139,10 +231,51 @@ static char *put_hex(char *o, const uint8_t *b, size_t n) {
 static void plugin_free(kbz_plugin_t *p) {
   if (!p) return;
   if (p->ctx) kbz_ctx_destroy(p->ctx);
+  for (size_t m = 0; m < p->nmod; m++) {
+    if (p->mctx && p->mctx[m]) kbz_ctx_destroy(p->mctx[m]);
+    if (p->mignore) free(p->mignore[m]);
+  }
+  free_strings(p->mod_names, p->nmod);
+  free(p->mctx);
+  free(p->mignore);
+  free(p->mvirgin);
+  free(p->mlast);
+  free(p->mnew);
+  free(p->mq);
+  free(p->mq_outcome);
+  free(p->r_mhnb);
   free(p->ignore);
   free(p->virgin);
   free(p->r_hnb);
   free(p);
+}
+
+/* per_module_coverage: module tables for the given names (taken over) */
+static int plugin_modules(kbz_plugin_t *p, char **names, size_t n) {
+  p->per_module = 1;
+  p->nmod = n;
+  p->mod_names = names;
+  const size_t m = p->map_size;
+  p->mctx = (kbz_ctx_t **)calloc(n, sizeof(kbz_ctx_t *));
+  p->mignore = (uint8_t **)calloc(n, sizeof(uint8_t *));
+  p->mvirgin = (uint8_t *)malloc(n * m);
+  p->mlast = (uint32_t *)calloc(n, sizeof(uint32_t));
+  p->mnew = (uint8_t *)calloc(n, 1);
+  p->mq = (uint8_t *)malloc(p->max_batch * n * m);
+  p->mq_outcome = (int8_t *)malloc(p->max_batch);
+  p->r_mhnb = (uint8_t *)malloc(n * p->max_batch);
+  if (!p->mctx || !p->mignore || !p->mvirgin || !p->mlast || !p->mnew || !p->mq ||
+      !p->mq_outcome || !p->r_mhnb) {
+    set_err("out of host memory");
+    return -1;
+  }
+  memset(p->mvirgin, 0xff, n * m);
+  return 0;
+}
+static long module_index(const kbz_plugin_t *p, const char *name) {
+  for (size_t i = 0; i < p->nmod; i++)
+    if (!strcmp(p->mod_names[i], name)) return (long)i;
+  return -1;
 }
 
 static kbz_plugin_t *plugin_alloc(int mode, size_t map_size, size_t max_batch) {
@@ -164,21 +297,26 @@ static kbz_plugin_t *plugin_alloc(int mode, size_t map_size, size_t max_batch) {
   return p;
 }
 
-static int load_ignore(kbz_plugin_t *p, const char *path) {
+static uint8_t *load_ignore_file(const char *path, size_t map_size) {
   FILE *f = fopen(path, "rb");
   if (!f) {
     set_err("Could not open ignore bytes file %s", path);
-    return -1;
+    return NULL;
   }
-  p->ignore = (uint8_t *)malloc(p->map_size);
-  size_t got = p->ignore ? fread(p->ignore, 1, p->map_size, f) : 0;
+  uint8_t *b = (uint8_t *)malloc(map_size);
+  size_t got = b ? fread(b, 1, map_size, f) : 0;
   const int extra = fgetc(f) != EOF;
   fclose(f);
-  if (got != p->map_size || extra) {
-    set_err("Incorrect size of ignore bytes file %s (need exactly %zu bytes)", path, p->map_size);
-    return -1;
+  if (got != map_size || extra) {
+    set_err("Incorrect size of ignore bytes file %s (need exactly %zu bytes)", path, map_size);
+    free(b);
+    return NULL;
   }
-  return 0;
+  return b;
+}
+static int load_ignore(kbz_plugin_t *p, const char *path) {
+  p->ignore = load_ignore_file(path, p->map_size);
+  return p->ignore ? 0 : -1;
 }
 
 static kbz_plugin_t *plugin_from_options(int mode, const char *options) {
@@ -197,6 +335,53 @@ static kbz_plugin_t *plugin_from_options(int mode, const char *options) {
   }
   kbz_plugin_t *p = plugin_alloc(mode, (size_t)m, (size_t)mb);
   if (!p) return NULL;
+  unsigned long long pm = 0;
+  if (mode == KBZ_MODE_DYNAMORIO && json_u64(options, "per_module_coverage", &pm) < 0) {
+    set_err("bad options (per_module_coverage must be an integer)");
+    plugin_free(p);
+    return NULL;
+  }
+  if (pm) {  /* dynamorio_instrumentation.c:1048-1063 */
+    size_t n = 0;
+    int bad = 0;
+    char **raw = json_array(options, "coverage_modules", &n, &bad);
+    if (bad || !n) {
+      free_strings(raw, n);
+      set_err("No Coverage Module selected, please specify one with the coverage_modules option.");
+      plugin_free(p);
+      return NULL;
+    }
+    char **names = (char **)calloc(n, sizeof(char *));
+    for (size_t i = 0; names && i < n; i++) names[i] = json_unquote(raw[i]);
+    free_strings(raw, n);
+    int ok = names != NULL;
+    for (size_t i = 0; ok && i < n; i++) ok = names[i] && *names[i];
+    if (!ok) {
+      free_strings(names, n);
+      set_err("coverage_modules must be an array of module names");
+      plugin_free(p);
+      return NULL;
+    }
+    if (plugin_modules(p, names, n)) {
+      plugin_free(p);
+      return NULL;
+    }
+    char *dir = json_str(options, "ignore_bytes_dir");  /* :802-814: <dir>/<module>.dat */
+    for (size_t i = 0; dir && i < n; i++) {
+      char path[4096];
+      snprintf(path, sizeof(path), "%s/%s.dat", dir, names[i]);
+      FILE *f = fopen(path, "rb");
+      if (!f) continue;  /* a module without a file has no ignore bytes */
+      fclose(f);
+      if (!(p->mignore[i] = load_ignore_file(path, p->map_size))) {
+        free(dir);
+        plugin_free(p);
+        return NULL;
+      }
+    }
+    free(dir);
+    return p;
+  }
   char *ign = mode == KBZ_MODE_DYNAMORIO ? json_str(options, "ignore_bytes_file") : NULL;
   if (ign) {
     const int rc = load_ignore(p, ign);
@@ -212,6 +397,25 @@ static kbz_plugin_t *plugin_from_options(int mode, const char *options) {
 /* a fresh state with the same configuration (merge results) */
 static kbz_plugin_t *plugin_clone_config(const kbz_plugin_t *src) {
   kbz_plugin_t *p = plugin_alloc(src->mode, src->map_size, src->max_batch);
+  if (p && src->per_module) {
+    char **names = (char **)calloc(src->nmod, sizeof(char *));
+    for (size_t i = 0; names && i < src->nmod; i++) names[i] = strdup(src->mod_names[i]);
+    int ok = names && !plugin_modules(p, names, src->nmod);
+    for (size_t i = 0; ok && i < src->nmod; i++) {
+      ok = names[i] != NULL;
+      if (ok && src->mignore[i]) {
+        ok = (p->mignore[i] = (uint8_t *)malloc(src->map_size)) != NULL;
+        if (ok) memcpy(p->mignore[i], src->mignore[i], src->map_size);
+      }
+    }
+    if (!ok) {
+      if (names && !p->mod_names) free_strings(names, src->nmod);
+      plugin_free(p);
+      set_err("out of host memory");
+      return NULL;
+    }
+    return p;
+  }
   if (p && src->ignore) {
     p->ignore = (uint8_t *)malloc(src->map_size);
     if (!p->ignore) {
@@ -225,7 +429,34 @@ static kbz_plugin_t *plugin_clone_config(const kbz_plugin_t *src) {
 }
 
 /* ---- GPU side ------------------------------------------------------------------------------ */
+static int ensure_module_ctxs(kbz_plugin_t *p) {
+  const size_t m = p->map_size;
+  uint8_t *v3 = (uint8_t *)malloc(3 * m);
+  if (!v3) {
+    set_err("out of host memory");
+    return -1;
+  }
+  memset(v3, 0xff, 3 * m);
+  for (size_t i = 0; i < p->nmod; i++) {
+    if (p->mctx[i]) continue;
+    p->mctx[i] = kbz_ctx_create(m, KBZ_MODE_DYNAMORIO, p->max_batch);
+    memcpy(v3, p->mvirgin + i * m, m);
+    if (!p->mctx[i] || kbz_set_virgin(p->mctx[i], v3) ||
+        kbz_set_last_hash(p->mctx[i], p->mlast[i]) ||
+        (p->mignore[i] && kbz_set_ignore(p->mctx[i], p->mignore[i]))) {
+      set_err("GPU context (module %s): %s", p->mod_names[i], kbz_last_error());
+      if (p->mctx[i]) kbz_ctx_destroy(p->mctx[i]);
+      p->mctx[i] = NULL;
+      free(v3);
+      return -1;
+    }
+  }
+  free(v3);
+  return 0;
+}
+
 static int ensure_ctx(kbz_plugin_t *p) {
+  if (p->per_module) return ensure_module_ctxs(p);
   if (p->ctx) return 0;
   p->ctx = kbz_ctx_create(p->map_size, p->mode, p->max_batch);
   if (!p->ctx) {
@@ -243,7 +474,28 @@ static int ensure_ctx(kbz_plugin_t *p) {
 }
 
 static int sync_mirror(kbz_plugin_t *p) {
-  if (!p->ctx || !p->mirror_stale) return 0;
+  if (!p->mirror_stale) return 0;
+  if (p->per_module) {
+    const size_t m = p->map_size;
+    uint8_t *v3 = (uint8_t *)malloc(3 * m);
+    if (!v3) {
+      set_err("out of host memory");
+      return -1;
+    }
+    for (size_t i = 0; i < p->nmod; i++) {
+      if (!p->mctx[i]) continue;
+      if (kbz_get_virgin(p->mctx[i], v3) || kbz_get_last_hash(p->mctx[i], &p->mlast[i])) {
+        set_err("GPU state download: %s", kbz_last_error());
+        free(v3);
+        return -1;
+      }
+      memcpy(p->mvirgin + i * m, v3, m);
+    }
+    free(v3);
+    p->mirror_stale = 0;
+    return 0;
+  }
+  if (!p->ctx) return 0;
   if (kbz_get_virgin(p->ctx, p->virgin) || kbz_get_last_hash(p->ctx, &p->last_hash)) {
     set_err("GPU state download: %s", kbz_last_error());
     return -1;
@@ -260,10 +512,20 @@ static int plugin_flush(kbz_plugin_t *p) {
   const size_t n = p->q_n;
   p->q_rows = NULL;
   p->q_n = 0;
-  if (kbz_ring_submit(p->ctx, n, 1, p->r_hnb, NULL, NULL, 0) || kbz_ring_flush(p->ctx)) {
+  if (p->per_module) {  /* has_new_coverage_per_module over the batch */
+    size_t offs[p->nmod];
+    for (size_t i = 0; i < p->nmod; i++) offs[i] = i * p->map_size;
+    if (kbz_triage_modules_host(p->mctx, p->nmod, p->mq, n, p->nmod * p->map_size, offs,
+                                p->mq_outcome, p->r_mhnb, p->r_hnb)) {
+      set_err("GPU triage: %s", kbz_last_error());
+      return -1;
+    }
+    for (size_t i = 0; i < p->nmod; i++) p->mnew[i] = p->r_mhnb[i * n + n - 1] != 0;
+  } else if (kbz_ring_submit(p->ctx, n, 1, p->r_hnb, NULL, NULL, 0) || kbz_ring_flush(p->ctx)) {
     set_err("GPU triage: %s", kbz_last_error());
     return -1;
   }
+  p->last_path_was_new = p->r_hnb[n - 1] != 0;
   p->r_base = p->q_base;
   p->r_n = n;
   p->q_base += (long)n;
@@ -281,6 +543,12 @@ static long plugin_record(kbz_plugin_t *p, const uint8_t *trace, int fuzz_result
     return -1;
   }
   if (p->q_rows && p->q_n == p->q_cap && plugin_flush(p)) return -1;
+  if (p->per_module && !p->q_rows) {  /* module maps back to back: nmod * map_size bytes */
+    if (ensure_ctx(p)) return -1;
+    p->q_rows = p->mq;
+    p->q_outcome = p->mq_outcome;
+    p->q_cap = p->max_batch;
+  }
   if (!p->q_rows) {  /* the exec's trace goes straight into pinned memory */
     if (ensure_ctx(p)) return -1;
     if (kbz_ring_acquire(p->ctx, &p->q_rows, &p->q_outcome, &p->q_cap)) {
@@ -290,7 +558,8 @@ static long plugin_record(kbz_plugin_t *p, const uint8_t *trace, int fuzz_result
     }
     if (p->q_cap > p->max_batch) p->q_cap = p->max_batch;
   }
-  memcpy(p->q_rows + p->q_n * p->map_size, trace, p->map_size);
+  const size_t row = (p->per_module ? p->nmod : 1) * p->map_size;
+  memcpy(p->q_rows + p->q_n * row, trace, row);
   /* the KBZ_FUZZ_* outcomes of kbz_triage.h use the same numbering */
   p->q_outcome[p->q_n] = (int8_t)fuzz_result;
   p->last_ticket = p->q_base + (long)p->q_n++;
@@ -315,13 +584,33 @@ static int plugin_result(kbz_plugin_t *p, long ticket) {
 static int plugin_triage_batch(kbz_plugin_t *p, const uint8_t *traces, size_t n, size_t stride,
                                const int8_t *outcome, uint8_t *hnb, uint32_t *h32,
                                uint64_t *x64) {
-  if (!p || (n && !traces) || stride < p->map_size) {
-    set_err("bad arguments (null traces or stride < map_size)");
+  const size_t row = p ? (p->per_module ? p->nmod : 1) * p->map_size : 0;
+  if (!p || (n && !traces) || stride < row) {
+    set_err("bad arguments (null traces or stride < the exec's map bytes)");
     return -1;
   }
   if (plugin_flush(p) || ensure_ctx(p)) return -1; /* queued execs come first */
-  const int want = (h32 ? KBZ_WANT_H32 : 0) | (x64 ? KBZ_WANT_X64 : 0);
   p->mirror_stale = 1;
+  if (p->per_module) {  /* hnb = the exec's result over all modules (0/1) */
+    if (h32 || x64) {
+      set_err("per_module_coverage: hashes are per module, not per exec");
+      return -1;
+    }
+    size_t offs[p->nmod];
+    for (size_t i = 0; i < p->nmod; i++) offs[i] = i * p->map_size;
+    for (size_t lo = 0; lo < n; lo += p->max_batch) {
+      const size_t cnt = n - lo < p->max_batch ? n - lo : p->max_batch;
+      if (kbz_triage_modules_host(p->mctx, p->nmod, traces + lo * stride, cnt, stride, offs,
+                                  outcome ? outcome + lo : NULL, p->r_mhnb,
+                                  hnb ? hnb + lo : p->r_hnb)) {
+        set_err("GPU triage: %s", kbz_last_error());
+        return -1;
+      }
+      for (size_t i = 0; i < p->nmod; i++) p->mnew[i] = p->r_mhnb[i * cnt + cnt - 1] != 0;
+    }
+    return 0;
+  }
+  const int want = (h32 ? KBZ_WANT_H32 : 0) | (x64 ? KBZ_WANT_X64 : 0);
   for (size_t lo = 0; lo < n; lo += p->max_batch) {
     const size_t cnt = n - lo < p->max_batch ? n - lo : p->max_batch;
     if (kbz_triage_batch_host(p->ctx, traces + lo * stride, cnt, stride,
@@ -343,22 +632,107 @@ static char *plugin_get_state(kbz_plugin_t *p) {
     return NULL;
   }
   if (plugin_flush(p) || sync_mirror(p)) return NULL;
-  const size_t m = p->map_size, k = nmaps(p);
-  char *s = (char *)malloc(256 + k * (2 * m + 32));
+  const size_t m = p->map_size, k = p->per_module ? p->nmod : nmaps(p);
+  size_t extra = 0;
+  for (size_t i = 0; p->per_module && i < p->nmod; i++) extra += 2 * strlen(p->mod_names[i]) + 128;
+  char *s = (char *)malloc(256 + k * (2 * m + 64) + extra);
   if (!s) {
     set_err("out of host memory");
     return NULL;
   }
+  /* last_process_status: the FUZZ_* result of the last exec (dynamorio_get_state :1249) */
   char *o = s + sprintf(s, "{\"map_size\":%zu", m);
-  for (size_t i = 0; i < k; i++) {
-    o += sprintf(o, ",\"%s\":\"", kMapNames[i]);
-    o = put_hex(o, p->virgin + i * m, m);
-    *o++ = '"';
+  if (p->mode == KBZ_MODE_DYNAMORIO)
+    o += sprintf(o, ",\"last_process_status\":%d", p->last_ticket >= 0 ? p->last_fuzz_result : 0);
+  if (p->per_module) {  /* dynamorio_get_state :1260-1275 */
+    o += sprintf(o, ",\"modules\":[");
+    for (size_t i = 0; i < p->nmod; i++) {
+      o += sprintf(o, "%s{\"name\":\"", i ? "," : "");
+      for (const char *c = p->mod_names[i]; *c; c++) {
+        if (*c == '"' || *c == '\\') *o++ = '\\';
+        *o++ = *c;
+      }
+      o += sprintf(o, "\",\"virgin_bits\":\"");
+      o = put_hex(o, p->mvirgin + i * m, m);
+      o += sprintf(o, "\",\"last_shm_hash\":%u,\"last_path_was_new\":%d}", p->mlast[i],
+                   p->mnew[i]);
+    }
+    *o++ = ']';
+  } else {
+    for (size_t i = 0; i < k; i++) {
+      o += sprintf(o, ",\"%s\":\"", kMapNames[i]);
+      o = put_hex(o, p->virgin + i * m, m);
+      *o++ = '"';
+    }
+    if (p->mode == KBZ_MODE_DYNAMORIO)
+      o += sprintf(o, ",\"last_shm_hash\":%u,\"last_path_was_new\":%d", p->last_hash,
+                   p->last_path_was_new);
   }
-  if (p->mode == KBZ_MODE_DYNAMORIO) o += sprintf(o, ",\"last_shm_hash\":%u", p->last_hash);
   *o++ = '}';
   *o = 0;
   return s;
+}
+
+static int set_state_modules(kbz_plugin_t *p, const char *json) {
+  size_t n = 0;
+  int bad = 0;
+  char **objs = json_array(json, "modules", &n, &bad);
+  if (bad || !objs) {
+    free_strings(objs, n);
+    set_err("state lacks a valid \"modules\" array");
+    return 1;
+  }
+  const size_t m = p->map_size;
+  uint8_t *v = (uint8_t *)malloc(p->nmod * m);
+  uint32_t *last = (uint32_t *)malloc(p->nmod * sizeof(uint32_t));
+  uint8_t *nw = (uint8_t *)malloc(p->nmod);
+  int rc = (!v || !last || !nw) ? (set_err("out of host memory"), 1) : 0;
+  if (!rc) {
+    memcpy(v, p->mvirgin, p->nmod * m);
+    memcpy(last, p->mlast, p->nmod * sizeof(uint32_t));
+    memcpy(nw, p->mnew, p->nmod);
+  }
+  for (size_t j = 0; !rc && j < n; j++) {  /* dynamorio_set_state :1330-1349: match by name */
+    char *name = json_str(objs[j], "name");
+    const long i = name ? module_index(p, name) : -1;
+    unsigned long long h = 0, lw = 0;
+    if (i < 0) {
+      set_err("state module %s is not a coverage module", name ? name : "(unnamed)");
+      rc = 1;
+    } else if (json_hex(objs[j], "virgin_bits", v + (size_t)i * m, m) ||
+               json_u64(objs[j], "last_shm_hash", &h) < 0 ||
+               json_u64(objs[j], "last_path_was_new", &lw) < 0) {
+      set_err("state module %s lacks valid virgin_bits / last_shm_hash", name);
+      rc = 1;
+    } else {
+      last[i] = (uint32_t)h;
+      nw[i] = lw != 0;
+    }
+    free(name);
+  }
+  uint8_t *v3 = rc ? NULL : (uint8_t *)malloc(3 * m);
+  if (!rc && !v3) rc = (set_err("out of host memory"), 1);
+  for (size_t i = 0; !rc && i < p->nmod; i++) {
+    if (!p->mctx[i]) continue;
+    memset(v3, 0xff, 3 * m);
+    memcpy(v3, v + i * m, m);
+    if (kbz_set_virgin(p->mctx[i], v3) || kbz_set_last_hash(p->mctx[i], last[i])) {
+      set_err("GPU state upload: %s", kbz_last_error());
+      rc = 1;
+    }
+  }
+  free(v3);
+  if (!rc) {
+    memcpy(p->mvirgin, v, p->nmod * m);
+    memcpy(p->mlast, last, p->nmod * sizeof(uint32_t));
+    memcpy(p->mnew, nw, p->nmod);
+    p->mirror_stale = 0;
+  }
+  free(v);
+  free(last);
+  free(nw);
+  free_strings(objs, n);
+  return rc;
 }
 
 static int plugin_set_state(kbz_plugin_t *p, const char *json) {
@@ -366,13 +740,18 @@ static int plugin_set_state(kbz_plugin_t *p, const char *json) {
     set_err("null argument");
     return 1;
   }
-  unsigned long long m = 0, h = 0;
+  unsigned long long m = 0, h = 0, lw = 0, ls = 0;
   if (json_u64(json, "map_size", &m) == 1 && m != p->map_size) {
     set_err("state map_size %llu does not match the plugin's %zu", m, p->map_size);
     return 1;
   }
   /* execs recorded before the new state was loaded belong to the old one */
   if (plugin_flush(p)) return 1;
+  if (json_u64(json, "last_process_status", &ls) < 0) {
+    set_err("bad last_process_status");
+    return 1;
+  }
+  if (p->per_module) return set_state_modules(p, json);
   const size_t ms = p->map_size, k = nmaps(p);
   uint8_t *v = (uint8_t *)malloc(3 * ms);
   if (!v) {
@@ -387,8 +766,9 @@ static int plugin_set_state(kbz_plugin_t *p, const char *json) {
       return 1;
     }
   }
-  if (p->mode == KBZ_MODE_DYNAMORIO && json_u64(json, "last_shm_hash", &h) < 0) {
-    set_err("bad last_shm_hash");
+  if (p->mode == KBZ_MODE_DYNAMORIO && (json_u64(json, "last_shm_hash", &h) < 0 ||
+                                        json_u64(json, "last_path_was_new", &lw) < 0)) {
+    set_err("bad last_shm_hash / last_path_was_new");
     free(v);
     return 1;
   }
@@ -400,6 +780,7 @@ static int plugin_set_state(kbz_plugin_t *p, const char *json) {
   memcpy(p->virgin, v, 3 * ms);
   free(v);
   p->last_hash = (uint32_t)h;
+  p->last_path_was_new = lw != 0;
   p->mirror_stale = 0;
   return 0;
 }
@@ -420,13 +801,20 @@ static kbz_plugin_t *plugin_merge_many(kbz_plugin_t **ps, size_t n) {
     return NULL;
   }
   for (size_t i = 0; i < n; i++) {
-    if (!ps[i] || ps[i]->mode != ps[0]->mode || ps[i]->map_size != ps[0]->map_size) {
-      set_err("states to merge must come from the same plugin with the same map_size");
+    int ok = ps[i] && ps[i]->mode == ps[0]->mode && ps[i]->map_size == ps[0]->map_size &&
+             ps[i]->per_module == ps[0]->per_module && ps[i]->nmod == ps[0]->nmod;
+    for (size_t j = 0; ok && j < ps[0]->nmod; j++)  /* dynamorio_merge :1190-1203 */
+      ok = module_index(ps[i], ps[0]->mod_names[j]) >= 0;
+    if (!ok) {
+      set_err("states to merge must come from the same plugin with the same map_size and "
+              "coverage modules");
       return NULL;
     }
     if (plugin_flush(ps[i]) || sync_mirror(ps[i])) return NULL;
   }
-  const size_t row = nmaps(ps[0]) * ps[0]->map_size;
+  const size_t m = ps[0]->map_size;
+  const size_t row = ps[0]->per_module ? m : nmaps(ps[0]) * m;
+  const size_t parts = ps[0]->per_module ? ps[0]->nmod : 1;
   uint8_t *rows = (uint8_t *)malloc(n * row);
   kbz_plugin_t *r = rows ? plugin_clone_config(ps[0]) : NULL;
   if (!r) {
@@ -434,15 +822,23 @@ static kbz_plugin_t *plugin_merge_many(kbz_plugin_t **ps, size_t n) {
     if (!rows) set_err("out of host memory");
     return NULL;
   }
-  for (size_t i = 0; i < n; i++) memcpy(rows + i * row, ps[i]->virgin, row);
-  const int rc = kbz_merge_and_host(r->virgin, rows, n, row);
-  free(rows);
-  if (rc) {
-    set_err("GPU merge: %s", kbz_last_error());
-    plugin_free(r);
-    return NULL;
+  for (size_t q = 0; q < parts; q++) {  /* one AND-fold per module (matched by name) */
+    for (size_t i = 0; i < n; i++) {
+      const uint8_t *src = ps[0]->per_module
+                               ? ps[i]->mvirgin + (size_t)module_index(ps[i], r->mod_names[q]) * m
+                               : ps[i]->virgin;
+      memcpy(rows + i * row, src, row);
+    }
+    uint8_t *dst = r->per_module ? r->mvirgin + q * m : r->virgin;
+    if (kbz_merge_and_host(dst, rows, n, row)) {
+      set_err("GPU merge: %s", kbz_last_error());
+      free(rows);
+      plugin_free(r);
+      return NULL;
+    }
   }
-  r->last_hash = 0; /* dynamorio_merge :1228; afl_merge starts everything but the maps fresh */
+  free(rows);
+  r->last_hash = 0; /* dynamorio_merge :1215-1228; afl_merge starts all but the maps fresh */
   return r;
 }
 
@@ -457,7 +853,11 @@ static const char kHelpDr[] =
     "Options:\n"
     "  map_size              Trace map size in bytes (default 65536)\n"
     "  max_batch             Execs triaged per GPU batch (default 4096)\n"
-    "  ignore_bytes_file     File of map_size bytes: nonzero bytes are ignored\n";
+    "  ignore_bytes_file     File of map_size bytes: nonzero bytes are ignored\n"
+    "  per_module_coverage   1: one map per coverage module (record() takes the modules'\n"
+    "                        maps back to back, in coverage_modules order)\n"
+    "  coverage_modules      Array of module names (per_module_coverage)\n"
+    "  ignore_bytes_dir      Directory of <module>.dat ignore bytes files (per_module_coverage)\n";
 
 static int plugin_help(int mode, char **help_str) {
   if (!help_str) return -1;

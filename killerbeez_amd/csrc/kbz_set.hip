@@ -230,6 +230,25 @@ int kbz_set_insert_device(kbz_set_t *s, const uint64_t *keys, const uint8_t *mas
   return 0;
 }
 
+int kbz_set_insert_host(kbz_set_t *s, const uint64_t *keys, size_t n, uint8_t *is_new_out) {
+  if (!s || (n && !keys)) return set_fail("null argument");
+  if (n == 0) return 0;
+  uint64_t *d_keys = nullptr;
+  uint8_t *d_new = nullptr;
+  int rc = set_fail("kbz_set_insert_host: device staging");
+  if (hipMalloc((void **)&d_keys, n * 16) == hipSuccess &&
+      hipMalloc((void **)&d_new, n) == hipSuccess &&
+      hipMemcpy(d_keys, keys, n * 16, hipMemcpyHostToDevice) == hipSuccess) {
+    rc = kbz_set_insert_device(s, d_keys, nullptr, n, d_new, nullptr);
+    if (!rc && (hipDeviceSynchronize() != hipSuccess ||
+                (is_new_out && hipMemcpy(is_new_out, d_new, n, hipMemcpyDeviceToHost) != hipSuccess)))
+      rc = set_fail("kbz_set_insert_host: copy out");
+  }
+  if (d_keys) (void)hipFree(d_keys);
+  if (d_new) (void)hipFree(d_new);
+  return rc;
+}
+
 // Insert every key of src into dst, in src's insertion order (device-only, stream-ordered).
 static int append_set(kbz_set_t *dst, const kbz_set_t *src, hipStream_t st) {
   const size_t nslots = src->mask + 1;

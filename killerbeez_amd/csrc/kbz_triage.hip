@@ -838,6 +838,7 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
 __device__ __forceinline__ int rows_differ(const uint8_t *x, const uint8_t *y, const uint8_t *ignore,
                                            uint32_t map_size) {
   int diff = 0;
+#pragma unroll 8  // independent iterations: 8 pairs of loads in flight per thread
   for (uint32_t i = threadIdx.x * 16; i < map_size; i += blockDim.x * 16) {
     const uint4 a = *(const uint4 *)(x + i), b = *(const uint4 *)(y + i);
     const uint64_t a0 = classify8((uint64_t)a.x | ((uint64_t)a.y << 32));
@@ -2533,6 +2534,54 @@ int kbz_triage_modules_device(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *t
     HIP_TRY(hipGetLastError());
   }
   return 0;
+}
+
+int kbz_triage_modules_host(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *traces, size_t n,
+                            size_t stride, const size_t *module_offsets, const int8_t *outcome,
+                            uint8_t *hnb_out, uint8_t *any_out) {
+  if (!ctxs || !k || !ctxs[0]) return fail("kbz_triage_modules_host: no modules");
+  if (n && (!traces || !hnb_out)) return fail("null argument");
+  if (stride & 15) return fail("kbz_triage_modules_host: stride must be a multiple of 16");
+  if (n == 0) return 0;
+  DevGuard g(ctxs[0]->device);
+  hipStream_t s = nullptr;
+  uint8_t *d_t = nullptr, *d_hnb = nullptr, *d_any = nullptr;
+  int8_t *d_oc = nullptr;
+  int rc = -1;
+  auto release = [&]() {
+    (void)hipStreamSynchronize(s);
+    if (d_t) (void)hipFree(d_t);
+    if (d_oc) (void)hipFree(d_oc);
+    if (d_hnb) (void)hipFree(d_hnb);
+    if (d_any) (void)hipFree(d_any);
+    if (s) (void)hipStreamDestroy(s);
+  };
+  do {
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void **)&d_t, n * stride) != hipSuccess ||
+        hipMalloc((void **)&d_hnb, k * n) != hipSuccess ||
+        hipMalloc((void **)&d_any, n) != hipSuccess ||
+        (outcome && hipMalloc((void **)&d_oc, n) != hipSuccess)) {
+      fail("kbz_triage_modules_host: device staging");
+      break;
+    }
+    if (hipMemcpyAsync(d_t, traces, n * stride, hipMemcpyHostToDevice, s) != hipSuccess ||
+        (outcome && hipMemcpyAsync(d_oc, outcome, n, hipMemcpyHostToDevice, s) != hipSuccess)) {
+      fail("kbz_triage_modules_host: copy in");
+      break;
+    }
+    if (kbz_triage_modules_device(ctxs, k, d_t, n, stride, module_offsets, d_oc, d_hnb, d_any, s))
+      break;
+    if (hipMemcpyAsync(hnb_out, d_hnb, k * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        (any_out && hipMemcpyAsync(any_out, d_any, n, hipMemcpyDeviceToHost, s) != hipSuccess)) {
+      fail("kbz_triage_modules_host: copy out");
+      break;
+    }
+    rc = 0;
+    for (size_t m = 0; m < k && !rc; m++) rc = kbz_sync(ctxs[m], s);
+  } while (0);
+  release();
+  return rc;
 }
 
 // ---- picker -----------------------------------------------------------------------------------

@@ -173,8 +173,15 @@ def state_maps(state_json: str, map_size: int) -> dict:
         if k in d:
             out[k] = np.frombuffer(bytes.fromhex(d[k]), np.uint8)
             assert out[k].size == map_size
-    if "last_shm_hash" in d:
-        out["last_shm_hash"] = int(d["last_shm_hash"])
+    for k in ("last_shm_hash", "last_path_was_new", "last_process_status"):
+        if k in d:
+            out[k] = int(d[k])
+    if "modules" in d:  # dynamorio per_module_coverage: {name: {virgin_bits, last_shm_hash, ...}}
+        out["modules"] = {m["name"]: {"virgin_bits": np.frombuffer(bytes.fromhex(m["virgin_bits"]),
+                                                                   np.uint8),
+                                      "last_shm_hash": int(m["last_shm_hash"]),
+                                      "last_path_was_new": int(m["last_path_was_new"])}
+                          for m in d["modules"]}
     return out
 
 
@@ -183,5 +190,13 @@ def state_json(maps: dict, map_size: int) -> str:
 
     d = {"map_size": map_size}
     for k, v in maps.items():
-        d[k] = int(v) if k == "last_shm_hash" else bytes(np.asarray(v, np.uint8)).hex()
+        if k == "modules":
+            d[k] = [{"name": name, "virgin_bits": bytes(np.asarray(m["virgin_bits"], np.uint8)).hex(),
+                     "last_shm_hash": int(m.get("last_shm_hash", 0)),
+                     "last_path_was_new": int(m.get("last_path_was_new", 0))}
+                    for name, m in v.items()]
+        elif k in ("last_shm_hash", "last_path_was_new", "last_process_status"):
+            d[k] = int(v)
+        else:
+            d[k] = bytes(np.asarray(v, np.uint8)).hex()
     return json.dumps(d)

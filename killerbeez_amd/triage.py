@@ -428,6 +428,14 @@ class UniqueSet:
         self._check(lib().kbz_set_keys(self._h, _np_ptr(out), n, C.byref(got)), "kbz_set_keys")
         return out[:got.value]
 
+    def insert_host(self, keys: np.ndarray) -> np.ndarray:
+        """Insert host keys uint64 [n, 2] in order (a state's key list being loaded); -> is_new."""
+        k = np.ascontiguousarray(keys, dtype=np.uint64).reshape(-1, 2)
+        out = np.zeros(max(k.shape[0], 1), np.uint8)
+        self._check(lib().kbz_set_insert_host(self._h, _np_ptr(k), k.shape[0], _np_ptr(out)),
+                    "kbz_set_insert_host")
+        return out[:k.shape[0]]
+
     def merge(self, other: "UniqueSet", stream=None) -> "UniqueSet":
         """A new set: the union of self and other, self's keys first (linux_ipt_merge,
         linux_ipt_instrumentation.c:944-978).  Neither input changes."""
@@ -445,3 +453,80 @@ def dedup_keys(x64, outcome):
     import torch
 
     return torch.stack([x64.to(torch.int64), outcome.to(torch.int64)], dim=1)
+
+
+class IptBatch:
+    """Intel-PT path keys for a batch of execs (kbz_ipt_*; linux_ipt_instrumentation.c
+    analyze_ipt :212-425): the host parser feeds TNT bits / TIP addresses per exec, the GPU
+    hashes every exec's two streams; novelty = UniqueSet insert-if-absent."""
+
+    def __init__(self, libraries=(), target=(0, 0)):
+        """libraries: [(start, end, hash32)] coverage libraries; target: (start, end) of the
+        executable (used when there are no libraries): add_tip_to_hash's ASLR adjustment."""
+        L = lib()
+        self._h = L.kbz_ipt_batch_create()
+        starts = np.array([l[0] for l in libraries], np.uint64)
+        ends = np.array([l[1] for l in libraries], np.uint64)
+        hashes = np.array([l[2] for l in libraries], np.uint32)
+        self._chk(L.kbz_ipt_set_ranges(self._h, len(libraries), _np_ptr(starts), _np_ptr(ends),
+                                       _np_ptr(hashes), int(target[0]), int(target[1])),
+                  "kbz_ipt_set_ranges")
+
+    @staticmethod
+    def _chk(rc, what):
+        if rc != 0:
+            raise KbzError(f"{what}: {(lib().kbz_ipt_last_error() or b'').decode()}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().kbz_ipt_batch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_tnt(self, bits: bytes, num_bits: int):
+        b = np.frombuffer(bytes(bits) + b"\0" * 8, np.uint8)
+        self._chk(lib().kbz_ipt_add_tnt(self._h, _np_ptr(b), int(num_bits)), "kbz_ipt_add_tnt")
+
+    def add_tip(self, tip: int):
+        self._chk(lib().kbz_ipt_add_tip(self._h, int(tip)), "kbz_ipt_add_tip")
+
+    def end_exec(self):
+        self._chk(lib().kbz_ipt_end_exec(self._h), "kbz_ipt_end_exec")
+
+    def feed(self, events):
+        """events uint64 [k, 3]: (0, bit bytes little endian, num_bits) / (1, tip, -) / (2, -, -)
+        = end of exec."""
+        for kind, a, b in np.asarray(events, np.uint64).reshape(-1, 3).tolist():
+            if kind == 0:
+                self.add_tnt(int(a).to_bytes(8, "little"), int(b))
+            elif kind == 1:
+                self.add_tip(int(a))
+            else:
+                self.end_exec()
+
+    def execs(self) -> int:
+        return lib().kbz_ipt_execs(self._h)
+
+    def hash_device(self, stream=None):
+        """-> CUDA int64 [n, 2] keys {tip, tnt} of the completed execs (the batch empties)."""
+        import torch
+
+        n = self.execs()
+        out = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+        self._chk(lib().kbz_ipt_hash_device(self._h, C.c_void_p(out.data_ptr()) if n else None,
+                                            _stream_handle(stream)), "kbz_ipt_hash_device")
+        return out
+
+    def triage(self, table: "UniqueSet"):
+        """-> (keys uint64 [n, 2], is_new uint8 [n]) on the host; the batch empties."""
+        n = self.execs()
+        keys = np.zeros((max(n, 1), 2), np.uint64)
+        isnew = np.zeros(max(n, 1), np.uint8)
+        self._chk(lib().kbz_ipt_triage(self._h, table._h, _np_ptr(keys), _np_ptr(isnew)),
+                  "kbz_ipt_triage")
+        return keys[:n], isnew[:n]

@@ -67,6 +67,9 @@ def lib():
         L.kbzo_xxh64.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
         L.kbzo_merge_and.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.kbzo_merge_many.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t]
+        L.kbzo_ipt_keys.restype = C.c_size_t
+        L.kbzo_ipt_keys.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p]
         L.kbzo_picker_ignore.restype = C.c_size_t
         L.kbzo_picker_ignore.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t,
                                          C.c_void_p, C.c_void_p]
@@ -114,6 +117,9 @@ def ref():
         R.ref_xxh64_ref.restype = C.c_uint64
         R.ref_xxh64_ref.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
         R.ref_xxh_version_ref.restype = C.c_uint
+        R.ref_ipt_keys_ref.restype = C.c_size_t
+        R.ref_ipt_keys_ref.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p]
         R.ref_picker_ignore_ref.restype = C.c_int
         R.ref_picker_ignore_ref.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                             C.c_void_p]
@@ -179,3 +185,18 @@ def picker_ignore(runs: np.ndarray):
     pc = np.zeros((files, max(iters - 1, 0)), np.uint32)
     tot = lib().kbzo_picker_ignore(_p(r), files, iters, size, _p(ign), _p(pc) if pc.size else None)
     return ign, pc, int(tot)
+
+
+def ipt_keys(events: np.ndarray, lib_starts=(), lib_ends=(), lib_hashes=(), target_start=0,
+             target_end=0, use_ref: bool = False) -> np.ndarray:
+    """Intel-PT path keys [execs, 2] = {tip, tnt} from events uint64 [k, 3] (kind, a, b): the
+    restatement, or the reference's own feeders (oracle/_ref) with use_ref."""
+    ev = np.ascontiguousarray(events, dtype=np.uint64).reshape(-1, 3)
+    ls = np.ascontiguousarray(lib_starts, dtype=np.uint64)
+    le = np.ascontiguousarray(lib_ends, dtype=np.uint64)
+    lh = np.ascontiguousarray(lib_hashes, dtype=np.uint32)
+    out = np.zeros((max(1, int((ev[:, 0] == 2).sum())), 2), np.uint64)
+    f = ref().ref_ipt_keys_ref if use_ref else lib().kbzo_ipt_keys
+    n = f(_p(ev), ev.shape[0], ls.size, _p(ls), _p(le), _p(lh), int(target_start),
+          int(target_end), _p(out))
+    return out[:n]

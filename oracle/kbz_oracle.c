@@ -393,3 +393,61 @@ size_t kbzo_picker_ignore(const uint8_t *runs, size_t files, size_t iters, size_
   }
   return total;
 }
+
+/* Intel-PT path keys (linux_ipt_instrumentation.c:110-189 feeders, :238-243 reset, :409-416
+ * digests), restated as two 8-byte word streams per exec hashed one-shot (XXH64's streaming and
+ * one-shot forms agree on the concatenated input):
+ *   TNT: packet bits are packed the reference's way -- bit i of a packet contributes
+ *        (byte & (1 << i%8)) << k, k = bits already packed -- and every 8 packed bits (the
+ *        `num_bits == sizeof(tnt_bits)` flush, :148) emit the word; at the end the partial word
+ *        (if any) and the total bit count;
+ *   TIP: every TIP address, ASLR-adjusted (:169-185): inside coverage library i ->
+ *        (tip - start_i) | hash_i << 32; else, without libraries, inside the target ->
+ *        tip - target_start; else unchanged.
+ * Events as ref_ipt_keys: (0, bit bytes, num_bits) TNT, (1, tip, -) TIP, (2, -, -) end of exec.
+ * keys_out[2e] = tip digest, [2e+1] = tnt digest.  Returns the number of execs. */
+size_t kbzo_ipt_keys(const uint64_t *ev, size_t n_ev, size_t nlib, const uint64_t *lib_starts,
+                     const uint64_t *lib_ends, const uint32_t *lib_hashes, uint64_t target_start,
+                     uint64_t target_end, uint64_t *keys_out) {
+  uint64_t *tnt = (uint64_t *)malloc((n_ev * 8 + 2) * sizeof(uint64_t));
+  uint64_t *tip = (uint64_t *)malloc((n_ev + 1) * sizeof(uint64_t));
+  size_t nt = 0, np = 0, execs = 0;
+  uint64_t bits = 0, nb = 0, total = 0;
+  for (size_t e = 0; e < n_ev; e++) {
+    const uint64_t kind = ev[3 * e], a = ev[3 * e + 1], b = ev[3 * e + 2];
+    if (kind == 0) {
+      for (uint64_t i = 0; i < b; i++) {
+        const unsigned byte = (unsigned)((a >> (8 * (i / 8))) & 0xff);
+        bits |= (uint64_t)((byte & (1u << (i % 8))) << nb);
+        if (++nb == 8) {
+          tnt[nt++] = bits;
+          bits = nb = 0;
+        }
+      }
+      total += b;
+    } else if (kind == 1) {
+      uint64_t adj = a;
+      if (nlib) {
+        for (size_t i = 0; i < nlib; i++)
+          if (lib_starts[i] <= a && a < lib_ends[i]) {
+            adj = (a - lib_starts[i]) | ((uint64_t)lib_hashes[i] << 32);
+            break;
+          }
+      } else if (target_start <= a && a < target_end) {
+        adj = a - target_start;
+      }
+      tip[np++] = adj;
+    } else {
+      if (nb) tnt[nt++] = bits;
+      tnt[nt++] = total;
+      keys_out[2 * execs] = kbzo_xxh64(tip, np * 8, 0);
+      keys_out[2 * execs + 1] = kbzo_xxh64(tnt, nt * 8, 0);
+      execs++;
+      nt = np = 0;
+      bits = nb = total = 0;
+    }
+  }
+  free(tnt);
+  free(tip);
+  return execs;
+}

@@ -58,6 +58,10 @@ void kbzo_merge_many(uint8_t *dest, const uint8_t *states, size_t n, size_t stat
  * returns the number of noisy bytes. */
 size_t kbzo_picker_ignore(const uint8_t *runs, size_t files, size_t iters, size_t size,
                           uint8_t *ignore, uint32_t *pair_counts);
+/* Intel-PT path keys {tip, tnt} per exec from an event list (see kbz_oracle.c). */
+size_t kbzo_ipt_keys(const uint64_t *ev, size_t n_ev, size_t nlib, const uint64_t *lib_starts,
+                     const uint64_t *lib_ends, const uint32_t *lib_hashes, uint64_t target_start,
+                     uint64_t target_end, uint64_t *keys_out);
 
 #ifdef __cplusplus
 }

@@ -18,6 +18,8 @@
  *             reference's own ignore_count / total_ignore_count instead of logging
  *   REF_HASH  afl_progs/hash.h:36-65 (hash32) and instrumentation/winafl_hash.h:80-112
  *             (hash32_with_ignore), instrumentation/xxhash.h + xxhash.c:855 (XXH64, v0.6.5)
+ *   REF_IPT   instrumentation/linux_ipt_instrumentation.c:26-43 + :110-189 (the Intel-PT TNT /
+ *             TIP streaming XXH64 feeders), over linux_ipt_instrumentation.h
  * MAP_SIZE is a compile-time constant in the reference (afl_progs/config.h:314-315); the
  * Makefile builds the 64 KiB and 1 MiB variants by defining it before the extracted code.
  */
@@ -138,6 +140,68 @@ unsigned long long REF_NAME(ref_xxh64)(const void *input, size_t len, unsigned l
   return XXH64(input, len, seed);
 }
 unsigned REF_NAME(ref_xxh_version)(void) { return XXH_versionNumber(); }
+#elif defined(REF_IPT)
+/* Intel-PT path hashing: the reference's own add_tnt_to_hash / add_tip_to_hash /
+ * finish_tnt_hash (instrumentation/linux_ipt_instrumentation.c:110-189, its IPT_DEBUG and
+ * BIT_TEST macros :26-43 with them), over its own state types (linux_ipt_instrumentation.h, which pulls in
+ * forkserver_internal.h, uthash.h and xxhash.h from the reference tree).  WARNING_MSG is the
+ * logging macro of the absent killerbeez-utils utils.h; its calls only report XXH_ERROR, which
+ * XXH64_update never returns for a valid state. */
+#define _GNU_SOURCE
+#include <linux/perf_event.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <sys/types.h>
+#include "linux_ipt_instrumentation.h"
+#define WARNING_MSG(...) ((void)0)
+#include "ipt_hash.inc"
+/* Events of one or more execs, as analyze_ipt (:212-425) feeds the hashes: kind 0 = TNT packet
+ * bits (a = up to 8 bit bytes, little endian; b = num_bits), kind 1 = TIP address a (before the
+ * ASLR adjustment), kind 2 = end of the exec -> keys_out[2e..2e+1] = {tip, tnt} digest, the
+ * ipt_hashtable_key of :409-416.  Each exec starts from the reset of :238-243. */
+size_t REF_NAME(ref_ipt_keys)(const uint64_t *ev, size_t n_ev, size_t nlib,
+                              uint64_t *lib_starts, uint64_t *lib_ends, uint32_t *lib_hashes,
+                              uint64_t target_start, uint64_t target_end, uint64_t *keys_out) {
+  linux_ipt_state_t st;
+  memset(&st, 0, sizeof(st));
+  st.num_coverage_libraries = nlib;
+  st.library_starts = lib_starts;
+  st.library_ends = lib_ends;
+  st.library_hashes = lib_hashes;
+  st.target_start = target_start;
+  st.target_end = target_end;
+  st.ipt_hashes.tnt = XXH64_createState();
+  st.ipt_hashes.tip = XXH64_createState();
+  size_t execs = 0;
+  int fresh = 1;
+  for (size_t e = 0; e < n_ev; e++) {
+    if (fresh) {  /* analyze_ipt :238-243 */
+      st.ipt_hashes.tnt_bits = 0;
+      st.ipt_hashes.num_bits = 0;
+      st.ipt_hashes.total_num_bits = 0;
+      XXH64_reset(st.ipt_hashes.tnt, 0);
+      XXH64_reset(st.ipt_hashes.tip, 0);
+      fresh = 0;
+    }
+    const uint64_t kind = ev[3 * e], a = ev[3 * e + 1], b = ev[3 * e + 2];
+    if (kind == 0) {
+      unsigned char bits[8];
+      memcpy(bits, &a, 8);
+      add_tnt_to_hash(&st.ipt_hashes, bits, (int)b);
+    } else if (kind == 1) {
+      add_tip_to_hash(&st, a);
+    } else {  /* :409-416 */
+      finish_tnt_hash(&st.ipt_hashes);
+      keys_out[2 * execs] = XXH64_digest(st.ipt_hashes.tip);
+      keys_out[2 * execs + 1] = XXH64_digest(st.ipt_hashes.tnt);
+      execs++;
+      fresh = 1;
+    }
+  }
+  XXH64_freeState(st.ipt_hashes.tnt);
+  XXH64_freeState(st.ipt_hashes.tip);
+  return execs;
+}
 #else
-#error "select one of REF_AFL / REF_DR / REF_PICKER / REF_HASH / REF_HASH_IGNORE / REF_XXH"
+#error "select one of REF_AFL / REF_DR / REF_PICKER / REF_HASH / REF_HASH_IGNORE / REF_XXH / REF_IPT"
 #endif

@@ -44,3 +44,16 @@ def test_plugin_library_exports_header():
     exported = _exported(kbuild.PLUGIN_LIB)
     assert not [f for f in declared if f not in exported]
     C.CDLL(kbuild.PLUGIN_LIB)
+
+
+def test_plugin_layout_matches_reference_header(tmp_path):
+    """tests/native/abi_layout.c: kbz_instrumentation_t against the reference's own
+    instrumentation/instrumentation.h (offsets, member types, appended members)."""
+    ref = "/root/reference/instrumentation"
+    if not os.path.exists(os.path.join(ref, "instrumentation.h")):
+        pytest.skip("reference tree absent")
+    exe = tmp_path / "abi_layout"
+    src = os.path.join(os.path.dirname(__file__), "native", "abi_layout.c")
+    subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Werror", "-I", ref, "-I", kbuild.INC,
+                           src, "-o", str(exe)])
+    assert subprocess.call([str(exe)]) == 0

@@ -212,3 +212,78 @@ def test_config1_real_traces_per_exec(gpu, name, mode):
             assert p.is_new_path() == int(exp[j] != 0), (tag, j)
             assert p.get_fuzz_result() == oc[j]
         p.close()
+
+
+# ---- dynamorio_gpu per_module_coverage (dynamorio_instrumentation.c:1048-1063, :1477-1493) ----
+
+MODS = ["target.exe", "lib_a.dll", "lib b.dll"]
+PM_OPTS = '{"map_size": %d, "max_batch": 16, "per_module_coverage": 1, "coverage_modules": %s}'
+
+
+def test_per_module_state_roundtrip_without_gpu():
+    import json
+
+    rng = np.random.default_rng(1239)
+    mods = {name: {"virgin_bits": rng.integers(0, 256, M).astype(np.uint8),
+                   "last_shm_hash": int(rng.integers(0, 2**32)), "last_path_was_new": i % 2}
+            for i, name in enumerate(MODS)}
+    opts = PM_OPTS % (M, json.dumps(MODS))
+    st = P.state_json({"last_process_status": 0, "modules": dict(reversed(list(mods.items())))}, M)
+    p = P.Plugin("dynamorio_gpu", opts, st)  # modules are matched by name, in any order
+    back = P.state_maps(p.get_state(), M)
+    assert list(back["modules"]) == MODS
+    for name, m in mods.items():
+        np.testing.assert_array_equal(back["modules"][name]["virgin_bits"], m["virgin_bits"])
+        assert back["modules"][name]["last_shm_hash"] == m["last_shm_hash"]
+        assert back["modules"][name]["last_path_was_new"] == m["last_path_was_new"]
+    bad = P.state_json({"modules": {"other.dll": mods[MODS[0]]}}, M)
+    assert p.set_state(bad) != 0 and "not a coverage module" in P.last_error()
+    with pytest.raises(RuntimeError, match="coverage_modules"):
+        P.Plugin("dynamorio_gpu", '{"map_size": %d, "per_module_coverage": 1}' % M)
+
+
+@pytest.mark.gpu
+def test_per_module_coverage_plugin(gpu, tmp_path):
+    """record() takes the modules' maps back to back; is_new_path = any module new; each module
+    keeps its own virgin map / ignore bytes (ignore_bytes_dir/<name>.dat) / last hash; state
+    dump -> load -> continue; merge ANDs module by module (matched by name)."""
+    import json
+
+    rng = np.random.default_rng(1477)
+    ign = np.where(rng.random(M) < 0.2, 0, 0xFF).astype(np.uint8)
+    (tmp_path / f"{MODS[1]}.dat").write_bytes(ign.tobytes())
+    opts = json.loads(PM_OPTS % (M, json.dumps(MODS)))
+    opts["ignore_bytes_dir"] = str(tmp_path)
+    opts = json.dumps(opts)
+    k, n = len(MODS), 120
+    parts = [synth.sparse_np(2 * n, M, seed=60 + i, hot_frac=0.05)[0] for i in range(k)]
+    for part in parts:
+        part[30:40] = part[29]
+    rows = np.concatenate(parts, axis=1)
+    igs = [None, ign, None]
+    p = P.Plugin("dynamorio_gpu", opts)
+    exp = [oracle.triage_batch(oracle.MODE_DYNAMORIO, parts[i][:n], None, ignore=igs[i])
+           for i in range(k)]
+    for j in range(n):
+        assert p.record(rows[j], P.FUZZ_NONE) == j
+        assert p.is_new_path() == int(any(e["hnb"][j] != 0 for e in exp)), j
+    st = p.get_state()
+    got = P.state_maps(st, M)["modules"]
+    for i, name in enumerate(MODS):
+        np.testing.assert_array_equal(got[name]["virgin_bits"], exp[i]["virgin"][0])
+        assert got[name]["last_shm_hash"] == exp[i]["last_hash"]
+        assert got[name]["last_path_was_new"] == int(exp[i]["hnb"][n - 1] != 0)
+    # dump -> load into a new state -> the next execs continue from it
+    q = P.Plugin("dynamorio_gpu", opts, st)
+    exp2 = [oracle.triage_batch(oracle.MODE_DYNAMORIO, parts[i][n:], None, ignore=igs[i],
+                                virgin=exp[i]["virgin"], last_hash=exp[i]["last_hash"])
+            for i in range(k)]
+    res = q.triage_batch(rows[n:], hashes=False)
+    np.testing.assert_array_equal(res["hnb"], np.any([e["hnb"] != 0 for e in exp2], axis=0))
+    # merge: module-wise AND
+    m = p.merge(q)
+    got = P.state_maps(m.get_state(), M)["modules"]
+    for i, name in enumerate(MODS):
+        np.testing.assert_array_equal(got[name]["virgin_bits"],
+                                      exp[i]["virgin"][0] & exp2[i]["virgin"][0])
+        assert got[name]["last_shm_hash"] == 0
