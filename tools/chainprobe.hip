@@ -87,5 +87,22 @@ int main() {
     printf("%-28s %6.1f cycles per step%s\n", names[v], (double)c[v] / steps,
            (v && __builtin_memcmp(ref[v], ref[0], sizeof(ref[0]))) ? "  RESULT MISMATCH" : "");
   }
+  // The config-3 floor: one 1 MiB trace is a chain of 131,072 steps; a batch of 16,384 traces
+  // is 256 waves of 64 chains.  Wall time of exactly that (pass 1's step form, keys from
+  // registers: no loads, no LDS), with 1 and 4 waves per CU.
+  const int chain_steps = 131072;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  for (int blocks : {256, 1024}) {
+    hipLaunchKernelGGL(chain<1>, dim3(blocks), dim3(64), 0, 0, ks, out, chain_steps, cyc);
+    (void)hipEventRecord(e0, 0);
+    hipLaunchKernelGGL(chain<1>, dim3(blocks), dim3(64), 0, 0, ks, out, chain_steps, cyc);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    printf("%d-step chains, %d waves of 64: %.3f ms\n", chain_steps, blocks, ms);
+  }
   return 0;
 }
