@@ -22,16 +22,17 @@ constexpr uint64_t kSimpleZero = 0x0101010101010101ULL;  // afl_instrumentation.
 
 KBZ_HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
 
-// count_class bucket of every byte (dynamorio_instrumentation.c:246-255), branch-free:
-// with hb = highest set bit of the byte, bucket = hb, doubled when 3 <= c <= 63
-// (hb in {4,8,16,32}, or c == 3 where hb == 2).
+// count_class bucket of every byte (dynamorio_instrumentation.c:246-255), branch-free in 13
+// instructions: the bucket is the highest set bit of z, where z moves bits 2-5 of the count c
+// up by one (c in 4..63 -> doubled) and gives c == 3 bit 2 (-> 4); c in {0, 1, 2} and
+// c >= 64 keep their own highest bit.
 KBZ_HD uint32_t classify4(uint32_t x) {
-  uint32_t s = x | ((x >> 1) & 0x7F7F7F7Fu);
+  const uint32_t x1 = x << 1, x2 = x << 2;  // (written so that it selects to 5 instructions)
+  const uint32_t z = (x | (x1 & 0x78787878u)) | (x2 & x1 & 0x04040404u);
+  uint32_t s = z | ((z >> 1) & 0x7F7F7F7Fu);  // smear each byte's highest bit downwards
   s |= (s >> 2) & 0x3F3F3F3Fu;
   s |= (s >> 4) & 0x0F0F0F0Fu;
-  const uint32_t hb = s & ~((s >> 1) & 0x7F7F7F7Fu);
-  const uint32_t e3 = x & (x >> 1) & (hb >> 1) & 0x01010101u;
-  return hb + (hb & 0x3C3C3C3Cu) + (e3 << 1);
+  return s ^ ((s >> 1) & 0x7F7F7F7Fu);
 }
 KBZ_HD uint64_t classify8(uint64_t x) {
   return (uint64_t)classify4((uint32_t)x) | ((uint64_t)classify4((uint32_t)(x >> 32)) << 32);
@@ -59,6 +60,25 @@ KBZ_HD uint64_t h32_mix(uint64_t k) {
   k = rotl64(k, 31);
   return k * kH32C2;
 }
+#if defined(__HIPCC__)
+// k * C mod 2^64 as one v_mad_u64_u32 (lo * C.lo, 64-bit) and two v_mul_lo_u32 for the cross
+// terms; the compiler's own lowering spends a fourth multiply (v_mul_hi_u32) on some of them.
+__device__ __forceinline__ uint64_t mul64_const(uint32_t lo, uint32_t hi, uint64_t c) {
+  uint64_t p, cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p), "=s"(cc) : "v"(lo), "s"((uint32_t)c));
+  (void)cc;
+  const uint32_t ph = (uint32_t)(p >> 32) + lo * (uint32_t)(c >> 32) + hi * (uint32_t)c;
+  return (p & 0xffffffffull) | ((uint64_t)ph << 32);
+}
+// h32_mix with 6 multiplies and the rotation as two v_alignbit.
+__device__ __forceinline__ uint64_t h32_mix_mad(uint64_t k) {
+  const uint64_t a = mul64_const((uint32_t)k, (uint32_t)(k >> 32), kH32C1);
+  const uint32_t al = (uint32_t)a, ah = (uint32_t)(a >> 32);
+  const uint32_t rl = __builtin_amdgcn_alignbit(al, ah, 1);  // rotl 31 = rotr 33
+  const uint32_t rh = __builtin_amdgcn_alignbit(ah, al, 1);
+  return mul64_const(rl, rh, kH32C2);
+}
+#endif
 KBZ_HD uint64_t h32_step(uint64_t h, uint64_t k) {
   h ^= k;
   h = rotl64(h, 27);

@@ -45,6 +45,10 @@ constexpr int kMaxSeg = 32;  // chunk segments for the column scan
 constexpr int kItemsPerCol = 8;
 
 enum { XF_RAW = 0, XF_CLASSIFY = 1, XF_SIMPLIFY = 2 };
+template <int V>
+struct IntC {  // a compile-time int passed to generic lambdas
+  static constexpr int value = V;
+};
 
 __host__ __device__ __forceinline__ int mode_nclass(int mode) {
   return mode == KBZ_MODE_DYNAMORIO ? 1 : 3;
@@ -117,6 +121,10 @@ __device__ __forceinline__ void vmcnt_wait() {
 // The same wait naming the ring slot's registers "+v" (cdna_hip_programming.md, asm loads form
 // (ii)): no consumer of them, a register copy included, is scheduled above it.
 template <int N>
+__device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[2]) {
+  asm volatile("s_waitcnt vmcnt(%2)" : "+v"(r[0]), "+v"(r[1]) : "n"(N) : "memory");
+}
+template <int N>
 __device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[4]) {
   asm volatile("s_waitcnt vmcnt(%4)"
                : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3])
@@ -178,7 +186,7 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 }
 #define KBZ_STAMP_DECL unsigned long long st_acc[4] = {0, 0, 0, 0}, st_t = stamp_now()
 #define KBZ_STAMP(i) do { const unsigned long long _n = stamp_now(); st_acc[i] += _n - st_t; st_t = _n; } while (0)
-#define KBZ_STAMP_FLUSH(slot) do { if ((threadIdx.x & 63) == 0 && (slot) < 8192) { for (int _i = 0; _i < 4; _i++) g_kbz_stamps[(slot) * 4 + _i] = st_acc[_i]; } } while (0)
+#define KBZ_STAMP_FLUSH(slot) do { if ((threadIdx.x & 63) == 0 && (slot) < 8192u) { for (int _i = 0; _i < 4; _i++) g_kbz_stamps[(slot) * 4 + _i] = st_acc[_i]; } } while (0)
 #else
 #define KBZ_STAMP_DECL do {} while (0)
 #define KBZ_STAMP(i) do {} while (0)
@@ -186,6 +194,17 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 #endif
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+// The same barrier written with builtins, so the compiler's wait-count pass sees that every LDS
+// operation issued before it is complete: after the inline-asm form it still waits lgkmcnt(0)
+// for loads whose results were already in registers, before the first use of any of them
+// (k_pass1w keeps a tile's words in registers across a barrier).  The empty asm statements are
+// compiler memory fences (the s_barrier builtin is not one).
+__device__ __forceinline__ void lds_barrier_seen() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // vmcnt(63) expcnt(7) lgkmcnt(0): LDS only
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 // streaming 16-B load of data read exactly once (nontemporal: do not keep it in L2)
 __device__ __forceinline__ uint4 ld_stream16(const uint8_t *p) {
@@ -206,6 +225,21 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
   if (xf == XF_SIMPLIFY) return b ? 0x80u : 0x01u;
   return b;
 }
+
+// k_pass1w shape (timing variants override them with -D): transform waves, loader waves, their
+// register ring depth, wave L's priority
+#ifndef KBZ_WIDE_NX
+#define KBZ_WIDE_NX 8
+#endif
+#ifndef KBZ_WIDE_NL
+#define KBZ_WIDE_NL 4
+#endif
+#ifndef KBZ_WIDE_D
+#define KBZ_WIDE_D 2
+#endif
+#ifndef KBZ_WIDE_LPRIO
+#define KBZ_WIDE_LPRIO 3
+#endif
 
 struct Pass1Args {
   const uint8_t *traces;
@@ -525,43 +559,46 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
 
 // ---------------------------------------------------------------------------------------------
 // pass 1, wide-map variant (few chunks: a batch of large maps, e.g. BASELINE config 3 with
-// 16,384 x 1 MiB = 256 chunks).  k_pass1s then runs one 2-wave workgroup per CU and is
-// compute-bound twice over (MI355X, config 3: 27.2 ms per batch; 9.3 ms without the transform
-// work, 3.3 ms with neither transform nor chains).  Here the per-word work is spread over
-// NX transform waves and the serial chain is cut to its dependent part:
-//   waves 0..NL-1 load 64/NL rows each of tile s into a D-deep register ring; wave 0 (L) also
-//                chains tile s-2: per word only the hash32 step (xor, rotl, *5+C) on the mixed
-//                word the X waves computed (+ XXH64 rounds);
-//   waves X_i:   transform tile s-1 COLUMN-wise: lane (w = lane % 32, half h = lane / 32) owns
-//                word w of the rows of row group g = 2 i + h (64 / (2 NX) consecutive rows).
-//                Per (row, word): classify / simplify (written back in place for XXH64), the
-//                hash32 mix k = h32_mix(word & ignore) into the k buffer, a plain per-lane OR
-//                per class, and the DynamoRIO neighbour test against the previous row of the
-//                same lane (a ballot per row; group boundaries are compared one step later
-//                through LDS).  The groups' ORs meet in LDS (ds_or_b64); X_0 stores them
-//                (chunk_or, segment atomics) one step later.  X waves issue no asm loads, so
-//                their stores disturb no counted wait.
-// A tile lives in buffer s % 3 for three steps (filled, transformed, chained); its k values in
-// kbuf[s % 3] with the tile's own swizzled [row][slot] layout, so the X writes (32 lanes per
-// row) and L's row-per-lane ds_read_b128 are both conflict-free.  Steps s = 0..ntiles+1,
-// rounded up to a multiple of D, one barrier each.  Same vmcnt accounting as k_pass1s for the
-// loaders (only their loads per step).  LDS ~106 KiB: one workgroup per CU, NL+NX waves.
+// 16,384 x 1 MiB = 256 chunks, one per CU).  k_pass1s would run one 2-wave workgroup per CU and
+// be compute-bound twice over (config 3: 27.2 ms per batch).  Here the per-word work is spread
+// over NX transform waves and the serial chain is cut to its dependent part:
+//   loaders  waves 0..NL-1 load 64/NL rows each of tile s into a D-deep register ring and store
+//            it to LDS at step s (NL = 4: two waves per chunk reach 4.8 TB/s on this pattern,
+//            four 6.0-6.2 TB/s, tools/widebw);
+//   L        wave 0 (also a loader, at raised priority) chains tile s-3: per word only the
+//            hash32 step (xor, rotl, *5+C) on the mixed word the X waves computed (+ XXH64);
+//   X_i      read tile s-1's words from LDS into registers at step s, transform them at step
+//            s+1 -- so no LDS latency is ever waited for before computing -- COLUMN-wise: lane
+//            (w = lane % 32, half h = lane / 32) owns word w of the rows of row group
+//            g = 2 i + h (64 / (2 NX) consecutive rows).  Per (row, word): classify / simplify,
+//            the hash32 mix k = h32_mix(word & ignore) into the k buffer (and the transformed
+//            word into twb for XXH64), a plain per-lane OR per class, the DynamoRIO neighbour
+//            test against the previous row of the same lane (one ballot per row; group
+//            boundaries are compared one step later through LDS).  The groups' ORs meet in LDS
+//            (ds_or_b64); X_0 stores them (chunk_or, segment atomics) one step later.  X waves
+//            issue no asm loads, so their stores disturb no counted wait.
+// Tile t: raw[t & 1] filled at step t and read at t+1; kbuf / twb[t & 1] written at t+2 and
+// chained at t+3; its ORs in orb[t & 1] from t+2 to t+3.  Steps s = 0..ntiles+2 rounded up to
+// a multiple of D, one barrier each (its lgkmcnt(0) completes every LDS read issued in the
+// step).  k values use the tile's swizzled [row][slot] layout, so the X writes (32 lanes per
+// row) and L's row-per-lane ds_read_b128 are both conflict-free.  Same vmcnt accounting as
+// k_pass1s for the loaders.  LDS 65 KiB (97 KiB with XXH64): one workgroup per CU.
 // ---------------------------------------------------------------------------------------------
-template <int MODE, bool IGN, bool X64, int NX, int NL, int D, bool ISO>
-__global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a) {
-  static_assert(NL == 2 || NL == 4, "64/NL rows per loader, 4 rows per wave-load");
-  static_assert(!ISO || (NL == 2 && NX == 8), "ISO layout: 11 waves");
+template <int MODE, bool IGN, bool X64, int NX, int NL, int D>
+__global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
+  static_assert(NL == 2 || NL == 4 || NL == 8, "64/NL rows per loader, 4 rows per wave-load");
   static_assert(kChunk % (2 * NX) == 0, "equal row groups");
   constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, RPW = kChunk / NL, NLD = RPW / RPI;
   constexpr int TILE = kChunk * SLOTS;  // uint4 per tile buffer
   constexpr int RG = kChunk / (2 * NX);  // rows per X row group
-  __shared__ uint4 lds[3 * TILE];
-  __shared__ uint4 kbuf[3 * TILE];             // k of each (row, word), same layout as lds
-  __shared__ uint64_t orb[3][NC][TW / 8];      // column ORs of the tile, per class
-  __shared__ uint64_t bnd[2][2 * NX][TW / 8];  // last row of each group (neighbour test)
+  __shared__ uint4 raw[2 * TILE];
+  __shared__ uint4 kbuf[2 * TILE];              // k of each (row, word), same layout as raw
+  __shared__ uint4 twb[X64 ? 2 * TILE : 1];     // transformed words (XXH64 input)
+  __shared__ uint64_t orb[2][NC][TW / 8];       // column ORs of the tile, per class
+  __shared__ uint64_t bnd[2][2 * NX][TW / 8];   // last row of each group (neighbour test)
   __shared__ uint64_t neqs[NX];
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: SGPR
   const int lane = threadIdx.x & 63;
   const uint32_t chunk = blockIdx.x;
   const uint64_t row0 = (uint64_t)chunk * kChunk;
@@ -570,51 +607,50 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
   const int oc = (valid && a.outcome) ? a.outcome[row0 + lane] : KBZ_FUZZ_NONE;
   const int cls = class_of(MODE, oc);
   const uint32_t ntiles = a.map_size / TW;
-  const uint32_t nsteps = ntiles + 2;
+  const uint32_t nsteps = ntiles + 3;
+  const uint32_t nb = (nsteps + D - 1) / D * D;  // steps (= barriers) of every wave
 
-  // Roles.  Default: waves 0..NL-1 load, wave 0 (L) also chains, the rest transform.  ISO (11
-  // waves, dispatched round-robin over the 4 SIMDs): L = wave 0 only chains, the loaders are
-  // waves 4 and 8, so L's SIMD runs no transform work (the chain is latency-bound and is the
-  // critical path of this kernel); X waves are 1-3, 5-7, 9-10.
-  const bool isL = wave == 0;
-  const bool isLd = ISO ? (wave == 4 || wave == 8) : wave < NL;
-  const int li = ISO ? (wave >> 3) : wave;
-  const int xrole = ISO ? wave - 1 - (wave > 4) - (wave > 8) : wave - NL;
-  if (isL || isLd) {
-    // ------------------------------------------------------------ loader waves and L
+  if (wave < NL) {
+    // ------------------------------------------------------------ loader waves (wave 0 = L)
+    const bool isL = wave == 0;
+    const int li = wave;
     const int lr = lane / SLOTS, ls = lane % SLOTS;
     const uint8_t *lbase = a.traces + row0 * a.stride + ls * 16;
     uint32_t roff[NLD];
 #pragma unroll
     for (int i = 0; i < NLD; i++)
       roff[i] = (uint32_t)(min(RPW * li + RPI * i + lr, nrows - 1) * a.stride);
-    auto load_half = [&](u32x4 (&r)[NLD], uint32_t t) {  // branch-free (see k_pass1s)
+    auto load_part = [&](u32x4 (&r)[NLD], uint32_t t) {  // branch-free (see k_pass1s)
       const uint32_t msk = t < ntiles ? ~0u : 0u;
 #pragma unroll
       for (int i = 0; i < NLD; i++) asm_load16(r[i], lbase + ((t * TW + roff[i]) & msk));
     };
-    auto store_half = [&](const u32x4 (&r)[NLD], int b) {
+    auto store_part = [&](const u32x4 (&r)[NLD], int b) {
 #pragma unroll
       for (int i = 0; i < NLD; i++) {
         const int rr = RPW * li + RPI * i + lr;
         const u32x4 v = r[i];
-        lds[b * TILE + rr * SLOTS + (ls ^ (rr & 15))] = make_uint4(v.x, v.y, v.z, v.w);
+        raw[b * TILE + rr * SLOTS + (ls ^ (rr & 15))] = make_uint4(v.x, v.y, v.z, v.w);
       }
     };
     uint64_t h = (uint64_t)(kHashConst ^ a.map_size);
     uint64_t x0 = kXP1 + kXP2, x1 = kXP2, x2 = 0, x3 = 0 - kXP1;
+    // all 16 slots of the lane's row are read first: one LDS wait per tile, then 32 steps
     auto chain_tile = [&](uint32_t t) {
-      const int b = t % 3;
-      const uint4 *krow = &kbuf[b * TILE + lane * SLOTS];
-      const uint4 *row = &lds[b * TILE + lane * SLOTS];
+      const int b = t & 1;
       const int sw = lane & 15;
-#pragma unroll 4
+      uint4 kk[SLOTS];
+#pragma unroll
+      for (int q = 0; q < SLOTS; q++) kk[q] = kbuf[b * TILE + lane * SLOTS + (q ^ sw)];
+#pragma unroll
       for (int q = 0; q < SLOTS; q++) {
-        const uint4 kk = krow[q ^ sw];
-        h = h32_step_fast(h, (uint64_t)kk.x | ((uint64_t)kk.y << 32));
-        h = h32_step_fast(h, (uint64_t)kk.z | ((uint64_t)kk.w << 32));
-        if (X64) {
-          const uint4 v = row[q ^ sw];  // transformed in place by the X waves
+        h = h32_step_fast(h, (uint64_t)kk[q].x | ((uint64_t)kk[q].y << 32));
+        h = h32_step_fast(h, (uint64_t)kk[q].z | ((uint64_t)kk[q].w << 32));
+      }
+      if (X64) {
+#pragma unroll 4
+        for (int q = 0; q < SLOTS; q++) {
+          const uint4 v = twb[b * TILE + lane * SLOTS + (q ^ sw)];
 #pragma unroll
           for (int e = 0; e < 2; e++) {
             const uint64_t tw = ld_u64(v, e);
@@ -627,35 +663,33 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
         }
       }
     };
-    if (isLd) {  // the whole ring lives inside this wave-uniform branch
+    {  // the whole ring lives inside this wave-uniform branch
+      if (isL) __builtin_amdgcn_s_setprio(KBZ_WIDE_LPRIO);  // the chain is the critical path
       u32x4 R[D][NLD];
 #pragma unroll
-      for (int d = 0; d < D; d++) load_half(R[d], d);
-      for (uint32_t g = 0; g < nsteps; g += D) {
+      for (int d = 0; d < D; d++) load_part(R[d], d);
+      KBZ_STAMP_DECL;
+      for (uint32_t g = 0; g < nb; g += D) {
 #pragma unroll
         for (int u = 0; u < D; u++) {
           const uint32_t s = g + u;
 #ifndef KBZ_XP_NOCHAIN
-          if (isL && s >= 2 && s - 2 < ntiles) chain_tile(s - 2);
+          if (isL && s >= 3 && s - 3 < ntiles) chain_tile(s - 3);
 #endif
+          KBZ_STAMP(0);
           vmcnt_wait_ring<(D - 1) * NLD>(R[u]);
-          store_half(R[u], s % 3);
-          load_half(R[u], s + D);
-          lds_barrier();
+          KBZ_STAMP(2);
+          store_part(R[u], s & 1);
+          load_part(R[u], s + D);
+          KBZ_STAMP(3);
+          lds_barrier_seen();
+          KBZ_STAMP(1);
         }
       }
+      KBZ_STAMP_FLUSH(chunk * 16 + wave);
       drain_asm_loads(R);
-    } else {  // ISO: L only chains
-      __builtin_amdgcn_s_setprio(3);
-      for (uint32_t g = 0; g < nsteps; g += D) {
-        for (int u = 0; u < D; u++) {
-          const uint32_t s = g + u;
-          if (s >= 2 && s - 2 < ntiles) chain_tile(s - 2);
-          lds_barrier();
-        }
-      }
     }
-    lds_barrier();  // (Z): the X waves' neighbour flags are in neqs
+    lds_barrier_seen();  // (Z): the X waves' neighbour flags are in neqs
     if (isL && valid) {
       const uint32_t h32 = h32_final(h);
       a.h32[row0 + lane] = h32;
@@ -673,7 +707,7 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
         a.shard_last[1] = 1;
       }
     }
-    if (isLd && li == 1 && MODE == KBZ_MODE_DYNAMORIO && valid) {
+    if (li == 1 && MODE == KBZ_MODE_DYNAMORIO && valid) {
       uint64_t nq = 0;
 #pragma unroll
       for (int i = 0; i < NX; i++) nq |= neqs[i];
@@ -681,7 +715,7 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
     }
   } else {
     // ------------------------------------------------------------ waves X_i (column-wise)
-    const int xi = xrole;
+    const int xi = wave - NL;
     const int w = lane & 31, hf = lane >> 5;
     const int grp = 2 * xi + hf;
     const int r0 = grp * RG;             // this lane's rows: r0 .. r0 + RG - 1
@@ -689,14 +723,19 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
     uint64_t present[NC];
 #pragma unroll
     for (int k = 0; k < NC; k++) present[k] = __ballot(valid && cls == k);
-    // 2-bit class code of each of this lane's rows (3: past the end of a partial chunk)
+    // 2-bit class code of each of this lane's rows.  A row past the end of a partial chunk
+    // holds a copy of the chunk's last row (the loaders clamp) and takes that row's class: OR-ing
+    // a copy into the class aggregate changes nothing, so no row needs masking.
     uint32_t clsw = 0;
+    if (NC > 1) {
 #pragma unroll
-    for (int i = 0; i < RG; i++) {
-      uint32_t c = 3;
+      for (int i = 0; i < RG; i++) {
+        const int r = min(r0 + i, nrows - 1);
+        uint32_t c = 0;
 #pragma unroll
-      for (int k = 0; k < NC; k++) c = ((present[k] >> (r0 + i)) & 1) ? (uint32_t)k : c;
-      clsw |= c << (2 * i);
+        for (int k = 1; k < NC; k++) c = ((present[k] >> r) & 1) ? (uint32_t)k : c;
+        clsw |= c << (2 * i);
+      }
     }
     if (xi == 0) {
       if (lane == 0) {
@@ -705,89 +744,128 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
         for (int k = 0; k < NC; k++) m |= present[k] ? (1u << k) : 0u;
         a.chunk_cls[chunk] = m;
       }
-      for (int i = lane; i < 3 * NC * (TW / 8); i += 64) (&orb[0][0][0])[i] = 0;
+      for (int i = lane; i < 2 * NC * (TW / 8); i += 64) (&orb[0][0][0])[i] = 0;
     }
     const uint32_t seg = chunk / a.seg_len;
     const uint64_t *igp = IGN ? (const uint64_t *)a.ignore + w : nullptr;
     uint64_t ig_next = IGN ? igp[0] : ~0ull;  // ignore word of the next tile (prefetched)
-    uint64_t nm = 0;                          // rows that differ from their predecessor
-    uint64_t ftw = 0, frel = ~0ull;           // first row's word / rel mask of the last tile
-    auto transform_tile = [&](uint32_t t) {
-      const int b = t % 3;
+    // per row i of this wave's two groups: OR over tiles of the ballot "differs from the row
+    // before" (wave-uniform: SGPR pairs, one s_or per row and tile); bit r of the chunk's neq
+    // mask comes from its half at the end
+    uint64_t nacc[RG];
+#pragma unroll
+    for (int i = 0; i < RG; i++) nacc[i] = 0;
+    uint64_t ftw = 0, frel = ~0ull;  // first row's word / rel mask of the last transformed tile
+    // byte offset of this lane's word in each of its rows, in tile buffer 0 (buffer b: + b TILE)
+    uint32_t adr[RG];
+#pragma unroll
+    for (int i = 0; i < RG; i++) {
+      const int r = r0 + i;
+      adr[i] = (uint32_t)(r * SLOTS + ((w >> 1) ^ (r & 15))) * 16u + (uint32_t)(w & 1) * 8u;
+    }
+    // words of two tiles in registers: xw[t & 1] holds tile t from its read (step t+1) to its
+    // transform (step t+2).  The step loop is unrolled by 2, so every buffer and register set
+    // index is a constant and each LDS access is a per-row base plus an immediate offset.
+    uint64_t xw[2][RG];
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+#pragma unroll
+      for (int i = 0; i < RG; i++) xw[j][i] = 0;
+    auto read_tile = [&](uint32_t t, auto bc) {
+      constexpr int b = decltype(bc)::value;  // t & 1
+      const char *tb = (const char *)&raw[b * TILE];
+#pragma unroll
+      for (int i = 0; i < RG; i++) xw[b][i] = *(const uint64_t *)(tb + adr[i]);
+    };
+    auto transform_tile = [&](uint32_t t, auto bc) {
+      constexpr int b = decltype(bc)::value;  // t & 1
       const uint64_t igw = ig_next;
       if (IGN) ig_next = igp[(size_t)min(t + 1, ntiles - 1) * (TW / 8)];
       const uint64_t rel = IGN ? ~nonzero_bytes8(igw) : ~0ull;
+      uint64_t tw[RG];
+#pragma unroll
+      for (int i = 0; i < RG; i++) {
+        tw[i] = xw[b][i];
+#ifdef KBZ_XP_NOCLS
+        if (MODE == KBZ_MODE_DYNAMORIO) continue;
+#endif
+        const uint32_t c = (clsw >> (2 * i)) & 3;
+        if (MODE == KBZ_MODE_DYNAMORIO) tw[i] = classify8(tw[i]);
+        else if (c != 0) tw[i] = simplify8(tw[i]);
+        else if (MODE == KBZ_MODE_AFL_CLASSIFY) tw[i] = classify8(tw[i]);
+      }
+      if (X64) {
+        char *xb = (char *)&twb[b * TILE];
+#pragma unroll
+        for (int i = 0; i < RG; i++) *(uint64_t *)(xb + adr[i]) = tw[i];
+      }
+      char *kb = (char *)&kbuf[b * TILE];
+#pragma unroll
+      for (int i = 0; i < RG; i++) {
+#ifdef KBZ_XP_NOMIX
+        *(uint64_t *)(kb + adr[i]) = tw[i] & igw;
+#else
+        *(uint64_t *)(kb + adr[i]) = h32_mix_mad(tw[i] & igw);
+#endif
+      }
       uint64_t ow[NC];
 #pragma unroll
       for (int k = 0; k < NC; k++) ow[k] = 0;
-      uint64_t prev = 0;
 #pragma unroll
       for (int i = 0; i < RG; i++) {
-        const int r = r0 + i;
-        const int ad = r * SLOTS + ((w >> 1) ^ (r & 15));
-        uint64_t *p = (uint64_t *)&lds[b * TILE + ad] + (w & 1);
-        const uint64_t x = *p;
-        const uint32_t c = (clsw >> (2 * i)) & 3;
-        uint64_t tw;
-#ifdef KBZ_XP_NOCLS
-        if (MODE == KBZ_MODE_DYNAMORIO) tw = x;
-#else
-        if (MODE == KBZ_MODE_DYNAMORIO) tw = classify8(x);
-#endif
-        else if (c == 1 || c == 2) tw = simplify8(x);
-        else tw = (MODE == KBZ_MODE_AFL_CLASSIFY) ? classify8(x) : x;
-        if (X64) *p = tw;
-#ifdef KBZ_XP_NOMIX
-        ((uint64_t *)&kbuf[b * TILE + ad])[w & 1] = tw & igw;
-#else
-        ((uint64_t *)&kbuf[b * TILE + ad])[w & 1] = h32_mix(tw & igw);
-#endif
+        if (NC == 1) {
+          ow[0] |= tw[i];
+        } else {
+          const uint32_t c = (clsw >> (2 * i)) & 3;
 #pragma unroll
-        for (int k = 0; k < NC; k++) ow[k] |= (c == (uint32_t)k) ? tw : 0;
-        if (MODE == KBZ_MODE_DYNAMORIO) {
-          if (i == 0) {
-            ftw = tw;
-          } else {
-            const uint64_t bal = __ballot(((tw ^ prev) & rel) != 0);
-            nm |= ((uint64_t)((uint32_t)bal != 0) << (r0a + i)) |
-                  ((uint64_t)((uint32_t)(bal >> 32) != 0) << (r0b + i));
-          }
-          prev = tw;
+          for (int k = 0; k < NC; k++) ow[k] |= (c == (uint32_t)k) ? tw[i] : 0;
         }
       }
       if (MODE == KBZ_MODE_DYNAMORIO) {
-        bnd[t & 1][grp][w] = prev;
+#pragma unroll
+        for (int i = 1; i < RG; i++) nacc[i] |= __ballot(((tw[i] ^ tw[i - 1]) & rel) != 0);
+        ftw = tw[0];
+        bnd[b][grp][w] = tw[RG - 1];
         frel = rel;
       }
 #pragma unroll
       for (int k = 0; k < NC; k++)
         if (present[k] && ow[k]) atomicOr((unsigned long long *)&orb[b][k][w], (unsigned long long)ow[k]);
     };
-    // one step after tile t was transformed: group-boundary neighbour test, and X_0 stores
-    // the tile's column ORs
+    // X_0: the virgin words of tile t, loaded into vpre[t & 1] at the end of step t+1, two
+    // steps before finish_tile(t) needs them
+    uint64_t vpre[2][NC];
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+#pragma unroll
+      for (int k = 0; k < NC; k++) vpre[j][k] = 0;
+    auto load_virgin = [&](uint32_t t, auto bc) {
+      constexpr int b = decltype(bc)::value;  // t & 1
+#pragma unroll
+      for (int k = 0; k < NC; k++)
+        if (present[k] && lane < TW / 8)
+          vpre[b][k] = *(const uint64_t *)(a.vcur + (size_t)k * a.map_size + (size_t)t * TW +
+                                          (size_t)lane * 8);
+    };
     uint64_t tfl[NC];  // X_0: stored-tile bits of the current 64-tile flag word (k_pass1s)
 #pragma unroll
     for (int k = 0; k < NC; k++) tfl[k] = 0;
     uint64_t *tfbase = a.tflags + (size_t)chunk * NC * a.nfw;
-    auto finish_tile = [&](uint32_t t) {
-      if (MODE == KBZ_MODE_DYNAMORIO) {
-        // group 0's first row is row 0: against 0, a placeholder k_skip does not use
-        const uint64_t pl = grp > 0 ? bnd[t & 1][grp - 1][w] : 0;
-        const uint64_t bal = __ballot(((ftw ^ pl) & frel) != 0);
-        nm |= ((uint64_t)((uint32_t)bal != 0) << r0a) |
-              ((uint64_t)((uint32_t)(bal >> 32) != 0) << r0b);
-      }
+    // one step after tile t was transformed: group-boundary neighbour test (pl = the previous
+    // group's last row, read at the start of the step), and X_0 stores the tile's column ORs
+    auto finish_tile = [&](uint32_t t, uint64_t pl, uint64_t fw, uint64_t fr, auto bc) {
+      constexpr int b = decltype(bc)::value;  // t & 1
+      if (MODE == KBZ_MODE_DYNAMORIO) nacc[0] |= __ballot(((fw ^ pl) & fr) != 0);
       if (xi == 0) {
         // like k_pass1s: chunk_or and the segment aggregate keep only the bits still virgin at
         // batch entry; a tile with none is not stored, its flag bit stays clear
-        const int b = t % 3;
 #pragma unroll
         for (int k = 0; k < NC; k++) {
           if (!present[k]) continue;
           const size_t off = (size_t)k * a.map_size + (size_t)t * TW + (size_t)(lane & 31) * 8;
           uint64_t m = 0;
           if (lane < TW / 8) {
-            m = orb[b][k][lane] & *(const uint64_t *)(a.vcur + off);
+            m = orb[b][k][lane] & vpre[b][k];
             orb[b][k][lane] = 0;
           }
           if (__ballot(m != 0)) {
@@ -804,16 +882,42 @@ __global__ __launch_bounds__(64 * (NL + NX + ISO), 1) void k_pass1w(Pass1Args a)
         }
       }
     };
-    for (uint32_t g = 0; g < nsteps; g += D) {
-      for (int u = 0; u < D; u++) {
-        const uint32_t s = g + u;
-        if (s >= 2 && s - 2 < ntiles) finish_tile(s - 2);
-        if (s >= 1 && s - 1 < ntiles) transform_tile(s - 1);
-        lds_barrier();
-      }
+    KBZ_STAMP_DECL;
+    auto step = [&](uint32_t s, auto pc) {
+      constexpr int p = decltype(pc)::value;  // s & 1
+      // (1) LDS reads, issued first and waited for only after the transform (the LDS queue is
+      // long right after the barrier, with every wave's fills, reads and writes): the previous
+      // group's last row of tile s-3, then the words of tile s-1 (transformed next step)
+      uint64_t pl = 0;
+      const bool fin = s >= 3 && s - 3 < ntiles;
+      if (MODE == KBZ_MODE_DYNAMORIO && fin && grp > 0) pl = bnd[p ^ 1][grp - 1][w];
+      if (s >= 1 && s - 1 < ntiles) read_tile(s - 1, IntC<p ^ 1>{});
+      const uint64_t fw = ftw, fr = frel;  // tile s-3's, from its transform at step s-1
+      KBZ_STAMP(2);
+      // (2) transform tile s-2 from the registers read at step s-1
+      if (s >= 2 && s - 2 < ntiles) transform_tile(s - 2, IntC<p>{});
+      KBZ_STAMP(0);
+      // (3) finish tile s-3
+      if (fin) finish_tile(s - 3, pl, fw, fr, IntC<p ^ 1>{});
+      // (4) X_0: virgin words of tile s-1 (finished at step s+2; vpre[p ^ 1] was last read by
+      // finish_tile(s-3) above)
+      if (xi == 0 && s >= 1 && s - 1 < ntiles) load_virgin(s - 1, IntC<p ^ 1>{});
+      KBZ_STAMP(3);
+      lds_barrier_seen();
+      KBZ_STAMP(1);
+    };
+    for (uint32_t s0 = 0; s0 < nb; s0 += 2) {
+      step(s0, IntC<0>{});
+      if (s0 + 1 < nb) step(s0 + 1, IntC<1>{});
     }
+    KBZ_STAMP_FLUSH(chunk * 16 + wave);
+    uint64_t nm = 0;  // rows that differ from their predecessor
+#pragma unroll
+    for (int i = 0; i < RG; i++)
+      nm |= ((uint64_t)((uint32_t)nacc[i] != 0u) << (r0a + i)) |
+            ((uint64_t)((uint32_t)(nacc[i] >> 32) != 0u) << (r0b + i));
     if (lane == 0) neqs[xi] = nm;
-    lds_barrier();  // (Z)
+    lds_barrier_seen();  // (Z)
   }
 }
 
@@ -1650,19 +1754,6 @@ void free_ctx(kbz_ctx *c) {
   delete c;
 }
 
-#ifndef KBZ_WIDE_NX
-#define KBZ_WIDE_NX 8
-#endif
-#ifndef KBZ_WIDE_NL
-#define KBZ_WIDE_NL 2
-#endif
-#ifndef KBZ_WIDE_D
-#define KBZ_WIDE_D 2
-#endif
-#ifndef KBZ_WIDE_ISO
-#define KBZ_WIDE_ISO 0
-#endif
-constexpr bool kWideISO = KBZ_WIDE_ISO;     // k_pass1w role layout (see there)
 constexpr int kWideNX = KBZ_WIDE_NX;        // transform waves of k_pass1w
 constexpr int kWideNL = KBZ_WIDE_NL;        // loader waves of k_pass1w
 constexpr int kWideD = KBZ_WIDE_D;          // their register ring depth
@@ -1703,8 +1794,8 @@ void launch_pass1(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s
   return launch_abl<MODE, IGN, X64, 0>(depth, a, chunks, s);
 #else
   if (pass1_is_wide(choice, chunks))
-    hipLaunchKernelGGL((k_pass1w<MODE, IGN, X64, kWideNX, kWideNL, kWideD, kWideISO>),
-                       dim3(chunks), dim3(64 * (kWideNL + kWideNX + kWideISO)), 0, s, a);
+    hipLaunchKernelGGL((k_pass1w<MODE, IGN, X64, kWideNX, kWideNL, kWideD>), dim3(chunks),
+                       dim3(64 * (kWideNL + kWideNX)), 0, s, a);
   else
     hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, 0, KBZ_PASS1_DEPTH>), dim3(chunks), dim3(128), 0,
                        s, a);

@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Diagnostic: run k_pass1w on BASELINE config 3 (16,384 dense x 1 MiB) with a -DKBZ_STAMPS
+build (KBZ_HIP_LIB=...) and print, per wave of the workgroup, the median cycles per launch in
+{work, barrier wait, vmcnt wait / finish, LDS fill}.  Not part of the product."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from killerbeez_amd import synth  # noqa: E402
+from killerbeez_amd._lib import lib  # noqa: E402
+from killerbeez_amd.triage import WANT_H32, TriageContext  # noqa: E402
+
+L = lib()
+f = L.kbz_debug_stamps
+f.argtypes = [C.c_void_p, C.c_size_t]
+n, M = 16384, 1 << 20
+t, oc = synth.dense_torch(n, M, device="cuda")
+ctx = TriageContext(M, 1, n)
+for _ in range(3):
+    ctx.triage(t, oc, WANT_H32)
+torch.cuda.synchronize()
+buf = np.zeros(4096 * 2 * 4, np.uint64)
+f(buf.ctypes.data_as(C.c_void_p), buf.size)
+st = buf.reshape(-1, 16, 4)[:256].astype(np.float64)  # [chunk][wave][phase]
+names = ["work|xform", "barrier", "vmcnt|reads", "fill|finish"]
+for w in range(16):
+    tot = st[:, w, :].sum(axis=1)
+    if np.median(tot) == 0:
+        continue
+    cols = "  ".join(f"{nm} {np.median(st[:, w, i]) / 1e6:7.3f}M" for i, nm in enumerate(names))
+    print(f"wave {w:2d}: total {np.median(tot) / 1e6:7.3f}M cycles  {cols}")
