@@ -121,6 +121,7 @@ int kbz_afl_gpu_triage_batch(void *state, const uint8_t *traces, size_t n, size_
                              const int8_t *outcome, uint8_t *hnb_out, uint32_t *h32_out,
                              uint64_t *x64_out);
 void *kbz_afl_gpu_merge_many(void **states, size_t n);
+void *kbz_afl_gpu_merge_files(char *options, const char *const *paths, size_t n);
 int kbz_afl_gpu_help(char **help_str);
 /* Deferred per-exec path.  record: queue one exec's RAW trace map (map_size bytes, copied)
  * with its FUZZ_* result; returns the exec's ticket (>= 0) or -1.  The queue is triaged as one
@@ -147,6 +148,7 @@ int kbz_dynamorio_gpu_triage_batch(void *state, const uint8_t *traces, size_t n,
                                    const int8_t *outcome, uint8_t *hnb_out, uint32_t *h32_out,
                                    uint64_t *x64_out);
 void *kbz_dynamorio_gpu_merge_many(void **states, size_t n);
+void *kbz_dynamorio_gpu_merge_files(char *options, const char *const *paths, size_t n);
 int kbz_dynamorio_gpu_help(char **help_str);
 long kbz_dynamorio_gpu_record(void *state, const uint8_t *trace_bits, int fuzz_result);
 int kbz_dynamorio_gpu_result(void *state, long ticket);

@@ -199,6 +199,15 @@ int kbz_merge_and_device(uint8_t *out, const uint8_t *states, size_t n, size_t s
                          void *stream);
 /* Host variant: streams host states (pageable or pinned) through the device. Synchronous. */
 int kbz_merge_and_host(uint8_t *out, const uint8_t *states, size_t n, size_t state_bytes);
+/* The same fold with the states produced in place: the library calls fill(user, dst, first,
+ * count) to write states [first, first + count) (state_bytes each, back to back) straight into
+ * pinned staging memory dst, on the calling thread, while the GPU copies and folds the previous
+ * slot (slots of up to 256 MiB).  fill returns 0, or non-zero to abort (the merge then fails).
+ * The merger's file loop (merger/merger.c:79-99: read_file + create + merge per state file)
+ * becomes one such call (kbz_*_gpu_merge_files in libkbz_plugin.so). */
+typedef int (*kbz_merge_fill_fn)(void *user, uint8_t *dst, size_t first, size_t count);
+int kbz_merge_and_fill(uint8_t *out, size_t n, size_t state_bytes, kbz_merge_fill_fn fill,
+                       void *user);
 
 /* ---- DynamoRIO per-module coverage ----------------------------------------------------------- */
 /* has_new_coverage_per_module (dynamorio_instrumentation.c:1477-1493) over an ordered batch: each

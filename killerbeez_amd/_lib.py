@@ -46,6 +46,7 @@ SIGNATURES = [
     ("kbz_or_reduce", _i, [_vp, _vp, _sz, _sz, _sz, _vp]),
     ("kbz_merge_and_device", _i, [_vp, _vp, _sz, _sz, _vp]),
     ("kbz_merge_and_host", _i, [_vp, _vp, _sz, _sz]),
+    ("kbz_merge_and_fill", _i, [_vp, _sz, _sz, _vp, _vp]),
     ("kbz_triage_modules_device", _i, [_vp, _sz, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp]),
     ("kbz_triage_modules_host", _i, [_vp, _sz, _vp, _sz, _sz, _vp, _vp, _vp, _vp]),
     ("kbz_picker_ignore_device", _i, [_vp, _sz, _sz, _sz, _vp, _vp, _vp, _vp]),

@@ -55,7 +55,7 @@ def build_plugin(force: bool = False, verbose: bool = False) -> str:
     if not all(os.path.exists(s) for s in PLUGIN_SOURCES):
         return ""
     if force or _stale(PLUGIN_LIB, PLUGIN_SOURCES + PLUGIN_HEADERS + [HIP_LIB]):
-        cmd = ["gcc", "-O2", "-fPIC", "-shared", "-Wall", "-std=c11", "-I", INC,
+        cmd = ["gcc", "-O2", "-fPIC", "-shared", "-Wall", "-std=gnu11", "-pthread", "-I", INC,
                *PLUGIN_SOURCES, "-L", PKG, "-lkbz_hip", "-Wl,-rpath,$ORIGIN",
                "-o", PLUGIN_LIB + ".tmp"]
         if verbose:

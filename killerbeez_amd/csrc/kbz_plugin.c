@@ -31,6 +31,7 @@
 #define _POSIX_C_SOURCE 200809L /* strdup under -std=c11 */
 #include "kbz_plugin.h"
 
+#include <pthread.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -842,6 +843,192 @@ static kbz_plugin_t *plugin_merge_many(kbz_plugin_t **ps, size_t n) {
   return r;
 }
 
+/* ---- merge of state files: the merger's file loop (merger/merger.c:79-99) as one GPU fold ---
+ * Each file holds one state as get_state writes it.  Worker threads read and hex-decode the
+ * files straight into the library's pinned staging slots (kbz_merge_and_fill), k maps of
+ * map_size bytes per state back to back (k = 3 for afl_gpu, 1 for dynamorio_gpu, the number of
+ * coverage modules with per_module_coverage, in coverage_modules order); the GPU folds one slot
+ * while the next is decoded.  The result is what merging the created states pairwise gives:
+ * the AND of the maps, everything else fresh (afl_merge :123-140, dynamorio_merge :1180-1231). */
+static int8_t g_hexv[256];
+static pthread_once_t g_hex_once = PTHREAD_ONCE_INIT;
+static void hex_table_init(void) {
+  for (int c = 0; c < 256; c++) g_hexv[c] = (int8_t)hexval((char)c);
+}
+/* n bytes from the 2n hex digits of the JSON string value at v (just past its opening quote) */
+static int hex_decode(const char *v, uint8_t *out, size_t n) {
+  for (size_t i = 0; i < n; i++) {
+    const int hi = g_hexv[(uint8_t)v[2 * i]];  /* -1 for a non-digit, the NUL included */
+    if (hi < 0) return -1;
+    const int lo = g_hexv[(uint8_t)v[2 * i + 1]];
+    if (lo < 0) return -1;
+    out[i] = (uint8_t)(hi << 4 | lo);
+  }
+  return v[2 * n] == '"' ? 0 : -1;
+}
+static int json_hex_fast(const char *json, const char *key, uint8_t *out, size_t n) {
+  const char *v = json_value(json, key);
+  if (!v || *v != '"') return -1;
+  return hex_decode(v + 1, out, n);
+}
+
+typedef struct {
+  const kbz_plugin_t *cfg;   /* options of the merge (mode, map_size, modules) */
+  const char *const *paths;
+  size_t row;                /* bytes per state row */
+  uint8_t *dst;              /* current slot */
+  size_t first, count, next;
+  pthread_mutex_t mu;
+  int failed;
+  char err[512];
+} files_job_t;
+
+static char *read_text_file(const char *path) {
+  FILE *f = fopen(path, "rb");
+  if (!f) return NULL;
+  char *buf = NULL;
+  if (fseek(f, 0, SEEK_END) == 0) {
+    const long len = ftell(f);
+    if (len > 0 && fseek(f, 0, SEEK_SET) == 0 && (buf = (char *)malloc((size_t)len + 1))) {
+      if (fread(buf, 1, (size_t)len, f) != (size_t)len) {
+        free(buf);
+        buf = NULL;
+      } else {
+        buf[len] = 0;
+      }
+    }
+  }
+  fclose(f);
+  return buf;
+}
+
+/* one file -> one row; returns 0 or writes a message to err */
+static int decode_state_file(const files_job_t *j, const char *path, uint8_t *row, char *err,
+                             size_t errn) {
+  const kbz_plugin_t *c = j->cfg;
+  const size_t m = c->map_size;
+  char *text = read_text_file(path);
+  if (!text) {
+    snprintf(err, errn, "Could not read instrumentation file or empty instrumentation file: %s",
+             path);
+    return -1;
+  }
+  unsigned long long ms = 0;
+  int rc = 0;
+  if (json_u64(text, "map_size", &ms) == 1 && ms != m) {
+    snprintf(err, errn, "%s: map_size %llu differs from the options' %zu", path, ms, m);
+    rc = -1;
+  } else if (c->per_module) {  /* dynamorio_set_state :1330-1349: modules matched by name */
+    size_t n = 0;
+    int bad = 0;
+    char **objs = json_array(text, "modules", &n, &bad);
+    uint8_t *seen = (uint8_t *)calloc(c->nmod, 1);
+    if (bad || !objs || !seen) {
+      snprintf(err, errn, "%s: state lacks a valid \"modules\" array", path);
+      rc = -1;
+    }
+    for (size_t q = 0; !rc && q < n; q++) {
+      char *name = json_str(objs[q], "name");
+      const long i = name ? module_index(c, name) : -1;
+      if (i < 0 || json_hex_fast(objs[q], "virgin_bits", row + (size_t)i * m, m)) {
+        snprintf(err, errn, "%s: module %s is not a coverage module or lacks virgin_bits", path,
+                 name ? name : "(unnamed)");
+        rc = -1;
+      } else {
+        seen[i] = 1;
+      }
+      free(name);
+    }
+    for (size_t i = 0; !rc && i < c->nmod; i++)
+      if (!seen[i]) {  /* dynamorio_merge :1190-1203 needs the same modules in every state */
+        snprintf(err, errn, "%s: state lacks coverage module %s", path, c->mod_names[i]);
+        rc = -1;
+      }
+    free(seen);
+    free_strings(objs, n);
+  } else {
+    for (size_t i = 0; !rc && i < nmaps(c); i++)
+      if (json_hex_fast(text, kMapNames[i], row + i * m, m)) {
+        snprintf(err, errn, "%s: state lacks a valid \"%s\" (%zu bytes as hex)", path,
+                 kMapNames[i], m);
+        rc = -1;
+      }
+  }
+  free(text);
+  return rc;
+}
+
+static void *files_worker(void *arg) {
+  files_job_t *j = (files_job_t *)arg;
+  char err[512];
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    const size_t i = j->failed ? j->count : j->next++;
+    pthread_mutex_unlock(&j->mu);
+    if (i >= j->count) return NULL;
+    if (decode_state_file(j, j->paths[j->first + i], j->dst + i * j->row, err, sizeof(err))) {
+      pthread_mutex_lock(&j->mu);
+      if (!j->failed) memcpy(j->err, err, sizeof(err));
+      j->failed = 1;
+      pthread_mutex_unlock(&j->mu);
+      return NULL;
+    }
+  }
+}
+
+static int fill_from_files(void *user, uint8_t *dst, size_t first, size_t count) {
+  files_job_t *j = (files_job_t *)user;
+  j->dst = dst;
+  j->first = first;
+  j->count = count;
+  j->next = 0;
+  enum { kMaxThreads = 16 };
+  pthread_t th[kMaxThreads];
+  size_t nt = count < kMaxThreads ? count : kMaxThreads, started = 0;
+  for (; started < nt; started++)
+    if (pthread_create(&th[started], NULL, files_worker, j)) break;
+  if (started == 0) files_worker(j);  /* no threads available: decode on the caller */
+  for (size_t t = 0; t < started; t++) pthread_join(th[t], NULL);
+  return j->failed;
+}
+
+static kbz_plugin_t *plugin_merge_files(int mode, const char *options, const char *const *paths,
+                                        size_t n) {
+  if (!paths || !n) {
+    set_err("nothing to merge");
+    return NULL;
+  }
+  for (size_t i = 0; i < n; i++)
+    if (!paths[i]) {
+      set_err("null path");
+      return NULL;
+    }
+  kbz_plugin_t *r = plugin_from_options(mode, options);
+  if (!r) return NULL;
+  pthread_once(&g_hex_once, hex_table_init);
+  const size_t k = r->per_module ? r->nmod : nmaps(r);
+  files_job_t j;
+  memset(&j, 0, sizeof(j));
+  j.cfg = r;
+  j.paths = paths;
+  j.row = k * r->map_size;
+  pthread_mutex_init(&j.mu, NULL);
+  uint8_t *out = (uint8_t *)malloc(j.row);
+  int rc = out ? kbz_merge_and_fill(out, n, j.row, fill_from_files, &j) : -1;
+  pthread_mutex_destroy(&j.mu);
+  if (rc) {
+    if (!out) set_err("out of host memory");
+    else if (j.failed) set_err("%s", j.err);
+    else set_err("GPU merge: %s", kbz_last_error());
+    free(out);
+    plugin_free(r);
+    return NULL;
+  }
+  memcpy(r->per_module ? r->mvirgin : r->virgin, out, j.row);
+  free(out);
+  return r;  /* last hashes 0, nothing queued: a fresh state with the merged maps */
+}
+
 static const char kHelpAfl[] =
     "afl_gpu - AFL bitmap triage (has_new_bits vs virgin_bits/tmout/crash) on the GPU\n"
     "Options:\n"
@@ -874,6 +1061,9 @@ static int plugin_help(int mode, char **help_str) {
     return (a && b) ? plugin_merge_many(v, 2) : (set_err("null state"), (void *)NULL);         \
   }                                                                                            \
   void *P##_merge_many(void **s, size_t n) { return plugin_merge_many((kbz_plugin_t **)s, n); } \
+  void *P##_merge_files(char *options, const char *const *paths, size_t n) {                   \
+    return plugin_merge_files(MODE, options, paths, n);                                        \
+  }                                                                                            \
   char *P##_get_state(void *s) { return plugin_get_state((kbz_plugin_t *)s); }                 \
   void P##_free_state(char *s) { free(s); }                                                    \
   int P##_set_state(void *s, char *json) { return plugin_set_state((kbz_plugin_t *)s, json); } \

@@ -240,6 +240,9 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #ifndef KBZ_WIDE_LPRIO
 #define KBZ_WIDE_LPRIO 3
 #endif
+#ifndef KBZ_WIDE_BAL
+#define KBZ_WIDE_BAL 1
+#endif
 
 struct Pass1Args {
   const uint8_t *traces;
@@ -557,6 +560,36 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   }
 }
 
+// k_pass1w row groups.  X wave xi transforms two groups of wide_rg(xi) consecutive rows (one
+// per half-wave); groups 2 xi and 2 xi + 1 in row order.  Balanced layout (NX = 8, NL = 4): the
+// workgroup's waves are dealt to the 4 SIMDs cyclically, so X_0 and X_4 share a SIMD with wave
+// L, whose hash chain takes about four row-words of that SIMD's issue per step: they get 3 and
+// 2 rows per group, the others 5 and 4 (9 row-words per SIMD per step, L included).
+template <int NX, int NL>
+__host__ __device__ constexpr int wide_rg(int xi) {
+  return (KBZ_WIDE_BAL && NX == 8 && NL == 4)
+             ? ((xi & 3) == 0 ? (xi < 4 ? 3 : 2) : (xi < 4 ? 5 : 4))
+             : kChunk / (2 * NX);
+}
+template <int NX, int NL>
+__host__ __device__ constexpr int wide_gstart(int g) {
+  int r = 0;
+  for (int i = 0; i < g; i++) r += wide_rg<NX, NL>(i / 2);
+  return r;
+}
+template <int NX, int NL>
+__host__ __device__ constexpr bool wide_groups_ok() {
+  return wide_gstart<NX, NL>(2 * NX) == kChunk;
+}
+// the RG a switch case instantiates: the case's own value where some wave uses it, else the
+// uniform size (keeps unused instantiations out of the binary)
+template <int NX, int NL>
+__host__ __device__ constexpr int wide_rg_or(int rg) {
+  for (int i = 0; i < NX; i++)
+    if (wide_rg<NX, NL>(i) == rg) return rg;
+  return kChunk / (2 * NX);
+}
+
 // ---------------------------------------------------------------------------------------------
 // pass 1, wide-map variant (few chunks: a batch of large maps, e.g. BASELINE config 3 with
 // 16,384 x 1 MiB = 256 chunks, one per CU).  k_pass1s would run one 2-wave workgroup per CU and
@@ -587,11 +620,10 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
 template <int MODE, bool IGN, bool X64, int NX, int NL, int D>
 __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
   static_assert(NL == 2 || NL == 4 || NL == 8, "64/NL rows per loader, 4 rows per wave-load");
-  static_assert(kChunk % (2 * NX) == 0, "equal row groups");
+  static_assert(kChunk % (2 * NX) == 0 && wide_groups_ok<NX, NL>(), "row groups cover the chunk");
   constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, RPW = kChunk / NL, NLD = RPW / RPI;
   constexpr int TILE = kChunk * SLOTS;  // uint4 per tile buffer
-  constexpr int RG = kChunk / (2 * NX);  // rows per X row group
   __shared__ uint4 raw[2 * TILE];
   __shared__ uint4 kbuf[2 * TILE];              // k of each (row, word), same layout as raw
   __shared__ uint4 twb[X64 ? 2 * TILE : 1];     // transformed words (XXH64 input)
@@ -716,10 +748,12 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
   } else {
     // ------------------------------------------------------------ waves X_i (column-wise)
     const int xi = wave - NL;
+    auto xwave = [&](auto rgc) {
+    constexpr int RG = decltype(rgc)::value;  // rows per group of this wave
     const int w = lane & 31, hf = lane >> 5;
     const int grp = 2 * xi + hf;
-    const int r0 = grp * RG;             // this lane's rows: r0 .. r0 + RG - 1
-    const int r0a = 2 * xi * RG, r0b = r0a + RG;  // first rows of the wave's two groups
+    const int r0 = wide_gstart<NX, NL>(grp);  // this lane's rows: r0 .. r0 + RG - 1
+    const int r0a = wide_gstart<NX, NL>(2 * xi), r0b = r0a + RG;  // the wave's two groups
     uint64_t present[NC];
 #pragma unroll
     for (int k = 0; k < NC; k++) present[k] = __ballot(valid && cls == k);
@@ -918,6 +952,13 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
             ((uint64_t)((uint32_t)(nacc[i] >> 32) != 0u) << (r0b + i));
     if (lane == 0) neqs[xi] = nm;
     lds_barrier_seen();  // (Z)
+    };
+    switch (wide_rg<NX, NL>(xi)) {  // wave-uniform
+      case 2: xwave(IntC<wide_rg_or<NX, NL>(2)>{}); break;
+      case 3: xwave(IntC<wide_rg_or<NX, NL>(3)>{}); break;
+      case 4: xwave(IntC<wide_rg_or<NX, NL>(4)>{}); break;
+      default: xwave(IntC<wide_rg_or<NX, NL>(5)>{}); break;
+    }
   }
 }
 
@@ -2554,13 +2595,15 @@ struct MergeStaging {
 };
 }  // namespace
 
-int kbz_merge_and_host(uint8_t *out, const uint8_t *states, size_t n, size_t state_bytes) {
-  if (!out || (!states && n)) return fail("null argument");
+int kbz_merge_and_fill(uint8_t *out, size_t n, size_t state_bytes, kbz_merge_fill_fn fill,
+                       void *user) {
+  if (!out || (!fill && n)) return fail("null argument");
   if (state_bytes == 0) return 0;
   if (n == 0) {
     memset(out, 0xff, state_bytes);
     return 0;
   }
+  // slots of up to 256 MiB: the caller fills slot b while the GPU copies and folds slot b ^ 1
   const size_t per = std::max<size_t>(1, (256u << 20) / state_bytes);
   const size_t cap = std::min(per, n);
   MergeStaging m;
@@ -2579,7 +2622,7 @@ int kbz_merge_and_host(uint8_t *out, const uint8_t *states, size_t n, size_t sta
     const int sl = (int)(b & 1);
     const size_t cnt = std::min(cap, n - lo);
     HIP_TRY(hipEventSynchronize(m.used[sl]));
-    memcpy(m.pin[sl], states + lo * state_bytes, cnt * state_bytes);
+    if (fill(user, m.pin[sl], lo, cnt)) return fail("kbz_merge_and_fill: the fill callback failed");
     HIP_TRY(hipMemcpyAsync(m.dst[sl], m.pin[sl], cnt * state_bytes, hipMemcpyHostToDevice, m.cs));
     HIP_TRY(hipEventRecord(m.copied[sl], m.cs));
     HIP_TRY(hipStreamWaitEvent(m.ws, m.copied[sl], 0));
@@ -2597,6 +2640,24 @@ int kbz_merge_and_host(uint8_t *out, const uint8_t *states, size_t n, size_t sta
   HIP_TRY(hipStreamSynchronize(m.ws));
   HIP_TRY(hipMemcpy(out, m.acc, state_bytes, hipMemcpyDeviceToHost));
   return 0;
+}
+
+namespace {
+struct HostRows {
+  const uint8_t *states;
+  size_t state_bytes;
+};
+int fill_from_host(void *user, uint8_t *dst, size_t first, size_t count) {
+  const HostRows *h = (const HostRows *)user;
+  memcpy(dst, h->states + first * h->state_bytes, count * h->state_bytes);
+  return 0;
+}
+}  // namespace
+
+int kbz_merge_and_host(uint8_t *out, const uint8_t *states, size_t n, size_t state_bytes) {
+  if (!out || (!states && n)) return fail("null argument");
+  HostRows h{states, state_bytes};
+  return kbz_merge_and_fill(out, n, state_bytes, fill_from_host, &h);
 }
 
 // ---- standalone hashes ---------------------------------------------------------------------------

@@ -21,6 +21,7 @@ _FN = {
     "cleanup": (None, [_vp]),
     "merge": (_vp, [_vp, _vp]),
     "merge_many": (_vp, [C.POINTER(_vp), _sz]),
+    "merge_files": (_vp, [C.c_char_p, C.POINTER(C.c_char_p), _sz]),
     "get_state": (C.c_void_p, [_vp]),
     "free_state": (None, [C.c_void_p]),
     "set_state": (_i, [_vp, C.c_char_p]),
@@ -161,6 +162,18 @@ class Plugin:
         if not h:
             raise RuntimeError(f"merge_many: {last_error()}")
         return Plugin(states[0].name, _handle=h)
+
+
+    @staticmethod
+    def merge_files(name: str, options: str | None, paths: list[str]) -> "Plugin":
+        """The merger's loop over state files (merger/merger.c:79-99) as one GPU fold: the
+        files are decoded straight into pinned staging memory by worker threads."""
+        arr = (C.c_char_p * max(1, len(paths)))(*[os.fsencode(x) for x in paths])
+        h = getattr(lib(), f"kbz_{name}_merge_files")(options.encode() if options else None, arr,
+                                                       len(paths))
+        if not h:
+            raise RuntimeError(f"merge_files: {last_error()}")
+        return Plugin(name, _handle=h)
 
 
 def state_maps(state_json: str, map_size: int) -> dict:

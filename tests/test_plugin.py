@@ -194,6 +194,81 @@ def test_state_load_continue_and_merge(gpu, name, mode):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,mode", MODES)
+def test_merge_files_like_the_merger(gpu, name, mode, tmp_path):
+    """merger <plugin> out in_1 ... in_n (merger/merger.c:79-99): n state files folded in one
+    GPU call (files decoded into pinned memory by worker threads), against the AND of the maps
+    and the pairwise merge; more files than one staging slot holds; errors like the merger's."""
+    rng = np.random.default_rng(7)
+    n = 2100 if name == "afl_gpu" else 5000  # > 256 MiB / (3 x 16 KiB): several slots for AFL
+    m = 16384
+    keys = ("virgin_bits", "virgin_tmout", "virgin_crash") if name == "afl_gpu" else ("virgin_bits",)
+    maps = {k: np.full((n, m), 0xFF, np.uint8) for k in keys}
+    paths = []
+    for i in range(n):
+        st = {}
+        for k in keys:
+            clear = rng.random(m) < 0.002
+            maps[k][i, clear] = rng.integers(0, 255, int(clear.sum()), dtype=np.uint8)
+            st[k] = maps[k][i]
+        if name == "dynamorio_gpu":
+            st["last_shm_hash"] = int(rng.integers(1, 2**32))
+        pth = tmp_path / f"state{i}.json"
+        pth.write_text(P.state_json(st, m))
+        paths.append(str(pth))
+    opts = f'{{"map_size": {m}}}'
+    merged = P.Plugin.merge_files(name, opts, paths)
+    got = P.state_maps(merged.get_state(), m)
+    for k in keys:
+        np.testing.assert_array_equal(got[k], np.bitwise_and.reduce(maps[k], axis=0))
+    if name == "dynamorio_gpu":
+        assert got["last_shm_hash"] == 0
+    # the pairwise fold of the merger gives the same maps
+    a = P.Plugin(name, opts, open(paths[0]).read())
+    for pth in paths[1:4]:
+        a = a.merge(P.Plugin(name, opts, open(pth).read()))
+    small = P.state_maps(P.Plugin.merge_files(name, opts, paths[:4]).get_state(), m)
+    for k in keys:
+        np.testing.assert_array_equal(small[k], P.state_maps(a.get_state(), m)[k])
+    # errors: a missing file, a file with the wrong map size, nothing to merge
+    with pytest.raises(RuntimeError, match="Could not read"):
+        P.Plugin.merge_files(name, opts, paths[:3] + [str(tmp_path / "nope.json")])
+    with pytest.raises(RuntimeError, match="map_size"):
+        P.Plugin.merge_files(name, '{"map_size": 8192}', paths[:2])
+    with pytest.raises(RuntimeError, match="nothing to merge"):
+        P.Plugin.merge_files(name, opts, [])
+
+
+@pytest.mark.gpu
+def test_merge_files_per_module(gpu, tmp_path):
+    """per_module_coverage states: modules matched by name in every file, module-wise AND."""
+    m, names = 4096, ["a.dll", "b.exe", "c.so"]
+    rng = np.random.default_rng(3)
+    opts = f'{{"map_size": {m}, "per_module_coverage": 1, "coverage_modules": ["a.dll", "b.exe", "c.so"]}}'
+    exp = {nm: np.full(m, 0xFF, np.uint8) for nm in names}
+    paths = []
+    for i in range(40):
+        mods = {}
+        for nm in reversed(names) if i % 2 else names:  # module order differs between files
+            v = np.full(m, 0xFF, np.uint8)
+            clear = rng.random(m) < 0.01
+            v[clear] = rng.integers(0, 255, int(clear.sum()), dtype=np.uint8)
+            exp[nm] &= v
+            mods[nm] = {"virgin_bits": v, "last_shm_hash": i, "last_path_was_new": 0}
+        pth = tmp_path / f"s{i}.json"
+        pth.write_text(P.state_json({"modules": mods}, m))
+        paths.append(str(pth))
+    got = P.state_maps(P.Plugin.merge_files("dynamorio_gpu", opts, paths).get_state(), m)
+    for nm in names:
+        np.testing.assert_array_equal(got["modules"][nm]["virgin_bits"], exp[nm])
+        assert got["modules"][nm]["last_shm_hash"] == 0
+    bad = tmp_path / "bad.json"
+    bad.write_text(P.state_json({"modules": {"a.dll": {"virgin_bits": exp["a.dll"]}}}, m))
+    with pytest.raises(RuntimeError, match="lacks coverage module"):
+        P.Plugin.merge_files("dynamorio_gpu", opts, paths[:2] + [str(bad)])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,mode", MODES)
 def test_config1_real_traces_per_exec(gpu, name, mode):
     """BASELINE config 1 through the plugin as fuzzer/main.c:374-385 drives it (one exec, then
     is_new_path): the real afl-gcc traces of corpus/afl_test (tests/golden/config1.npz), whose
