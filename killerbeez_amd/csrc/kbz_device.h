@@ -22,17 +22,46 @@ constexpr uint64_t kSimpleZero = 0x0101010101010101ULL;  // afl_instrumentation.
 
 KBZ_HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
 
-// count_class bucket of every byte (dynamorio_instrumentation.c:246-255), branch-free in 13
-// instructions: the bucket is the highest set bit of z, where z moves bits 2-5 of the count c
-// up by one (c in 4..63 -> doubled) and gives c == 3 bit 2 (-> 4); c in {0, 1, 2} and
-// c >= 64 keep their own highest bit.
+KBZ_HD uint32_t bitrev32(uint32_t x) {
+#if defined(__clang__)
+  return __builtin_bitreverse32(x);  // v_bfrev_b32
+#else
+  x = ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
+  x = ((x >> 2) & 0x33333333u) | ((x & 0x33333333u) << 2);
+  x = ((x >> 4) & 0x0F0F0F0Fu) | ((x & 0x0F0F0F0Fu) << 4);
+  x = ((x >> 8) & 0x00FF00FFu) | ((x & 0x00FF00FFu) << 8);
+  return (x >> 16) | (x << 16);
+#endif
+}
+
+// count_class bucket of every byte (dynamorio_instrumentation.c:246-255), branch-free in 9
+// instructions on gfx950: the bucket is the highest set bit of z, where z moves bits 2-5 of the
+// count c up by one (c in 4..63 -> doubled), gives c == 3 bit 2 (-> 4) and sets bit 0 of every
+// byte (a sentinel: no byte of z is 0).  The highest set bit is the lowest set bit of the
+// bit-reversed word, r & -r per byte; with every byte of r >= 0x80, -r per byte is one 32-bit
+// subtraction with no borrow between bytes.  The sentinel alone (c == 0) is masked at the end.
+// (The round-1 form, a 3-step smear of the highest bit, was 13 instructions:
+// tools/valuprobe.hip.)
 KBZ_HD uint32_t classify4(uint32_t x) {
-  const uint32_t x1 = x << 1, x2 = x << 2;  // (written so that it selects to 5 instructions)
-  const uint32_t z = (x | (x1 & 0x78787878u)) | (x2 & x1 & 0x04040404u);
-  uint32_t s = z | ((z >> 1) & 0x7F7F7F7Fu);  // smear each byte's highest bit downwards
+#ifdef KBZ_CLASSIFY_SMEAR  // timing-only A/B builds (scripts/build_variants.sh): the 13-instruction form
+  const uint32_t y1 = x << 1, y2 = x << 2;
+  const uint32_t y = (x | (y1 & 0x78787878u)) | (y2 & y1 & 0x04040404u);
+  uint32_t s = y | ((y >> 1) & 0x7F7F7F7Fu);
   s |= (s >> 2) & 0x3F3F3F3Fu;
   s |= (s >> 4) & 0x0F0F0F0Fu;
   return s ^ ((s >> 1) & 0x7F7F7F7Fu);
+#endif
+  const uint32_t x1 = (x << 1) | 0x01010101u;                 // v_lshl_or_b32
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t m;  // one v_and_or_b32 (the compiler emits v_and + v_or); one SGPR operand at most
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(m) : "v"(x << 2), "s"(0x04040404u), "v"(0x79797979u));
+#else
+  const uint32_t m = ((x << 2) & 0x04040404u) | 0x79797979u;
+#endif
+  const uint32_t z = x | (x1 & m);                            // v_and_or_b32
+  const uint32_t r = bitrev32(z);
+  const uint32_t l = r & (0x01010100u - r);                   // v_sub, v_and
+  return bitrev32(l) & (x | 0xFEFEFEFEu);                     // v_bfrev, v_bitop3
 }
 KBZ_HD uint64_t classify8(uint64_t x) {
   return (uint64_t)classify4((uint32_t)x) | ((uint64_t)classify4((uint32_t)(x >> 32)) << 32);

@@ -60,18 +60,21 @@ void run(const unsigned char *p, size_t n, size_t M, size_t S, unsigned *o) {
 
 int main(int argc, char **argv) {
   const size_t n = 65536, M = 65536;
-  const size_t pads[] = {0, 256, 4096};
+  const size_t pads[] = {0, 256, 512, 4096 + 256};
   unsigned char *p;
   unsigned *o;
-  if (hipMalloc(&p, n * (M + 4096)) || hipMalloc(&o, 4)) return 1;
-  (void)hipMemset(p, 1, n * (M + 4096));
+  if (hipMalloc(&p, n * (M + 4096 + 256)) || hipMalloc(&o, 4)) return 1;
+  (void)hipMemset(p, 1, n * (M + 4096 + 256));
   for (size_t pad : pads) {
     const size_t S = M + pad;
     run<256, 2, 2>(p, n, M, S, o);
+    run<256, 4, 2>(p, n, M, S, o);
+    run<256, 2, 4>(p, n, M, S, o);
     run<512, 2, 2>(p, n, M, S, o);
     run<1024, 2, 2>(p, n, M, S, o);
   }
   run<256, 1, 1>(p, n, M, M, o);
   run<256, 2, 1>(p, n, M, M, o);
+  run<256, 4, 1>(p, n, M, M, o);
   return 0;
 }

@@ -20,6 +20,15 @@ __device__ __forceinline__ uint32_t cls4_old(uint32_t x) {
   const uint32_t e3 = x & (x >> 1) & (hb >> 1) & 0x01010101u;
   return hb + (hb & 0x3C3C3C3Cu) + (e3 << 1);
 }
+// the 13-instruction smear form (round 2 until the bit-reverse form replaced it)
+__device__ __forceinline__ uint32_t cls4_smear(uint32_t x) {
+  const uint32_t x1 = x << 1, x2 = x << 2;
+  const uint32_t z = (x | (x1 & 0x78787878u)) | (x2 & x1 & 0x04040404u);
+  uint32_t s = z | ((z >> 1) & 0x7F7F7F7Fu);
+  s |= (s >> 2) & 0x3F3F3F3Fu;
+  s |= (s >> 4) & 0x0F0F0F0Fu;
+  return s ^ ((s >> 1) & 0x7F7F7F7Fu);
+}
 __device__ __forceinline__ uint64_t mix_default(uint64_t k) { return h32_mix(k); }
 __device__ __forceinline__ uint64_t mix_mad(uint64_t k) { return h32_mix_mad(k); }
 
@@ -45,10 +54,19 @@ __global__ __launch_bounds__(512) void probe(const uint32_t *in, uint32_t *out, 
       if (V == 3) asm volatile("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x6c" : "+v"(a[i]) : "s"(s));
       if (V == 4) asm volatile("v_lshl_add_u64 v[0:1], v[0:1], 2, v[0:1]" ::: "v0", "v1");
       if (V == 5) asm volatile("v_alignbit_b32 %0, %0, %0, 5" : "+v"(a[i]));
+      if (V == 10) asm volatile("v_perm_b32 %0, %1, %0, %0" : "+v"(a[i]) : "s"(s));
+      if (V == 11) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a[i]) : "s"(s));
+      if (V == 12) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(a[i]) : "s"(s));
+      if (V == 13) asm volatile("v_mad_u32_u24 %0, %0, %1, %0" : "+v"(a[i]) : "s"(s));
+      if (V == 15) asm volatile("v_bfrev_b32 %0, %0" : "+v"(a[i]));
     }
     if (V == 6) {  // classify4, current SWAR form, 8 independent dwords
 #pragma unroll
       for (int i = 0; i < 8; i++) a[i] = cls4_old(a[i]) ^ s;
+    }
+    if (V == 14) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) a[i] = cls4_smear(a[i]) ^ s;
     }
     if (V == 7) {
 #pragma unroll
@@ -83,15 +101,17 @@ int main() {
   for (int i = 0; i < 4096; i++) h[i] = 0x9e3779b9u * (i + 7);
   (void)hipMemcpy(in, h, sizeof(h), hipMemcpyHostToDevice);
   kfn ks[] = {probe<0>, probe<1>, probe<2>, probe<3>, probe<4>, probe<5>, probe<6>, probe<7>,
-              probe<8>, probe<9>};
+              probe<8>, probe<9>, probe<10>, probe<11>, probe<12>, probe<13>, probe<14>, probe<15>};
   const char *names[] = {"v_mul_lo_u32", "v_mul_hi_u32", "v_mad_u64_u32", "v_bitop3_b32",
                          "v_lshl_add_u64", "v_alignbit_b32", "classify4 (round-1 form)",
-                         "classify4 (z form)", "h32_mix (compiler)", "h32_mix (mad form)"};
+                         "classify4 (bitrev form)", "h32_mix (compiler)", "h32_mix (mad form)",
+                         "v_perm_b32", "v_mul_u32_u24", "v_xor_b32", "v_mad_u32_u24",
+                         "classify4 (smear form)", "v_bfrev_b32"};
   // per-"unit": ops 0-5: one instruction of 8 chains; 6-7: one dword classified (8 per iter);
   // 8-9: one 64-bit word mixed (4 per iter)
-  const int per_iter[] = {8, 8, 8, 8, 8, 8, 8, 8, 4, 4};
+  const int per_iter[] = {8, 8, 8, 8, 8, 8, 8, 8, 4, 4, 8, 8, 8, 8, 8, 8};
   for (int w = 1; w <= 2; w++) {  // waves per SIMD: block of 256*w threads, 1 block per CU
-    for (int v = 0; v < 10; v++) {
+    for (int v = 0; v < 16; v++) {
       unsigned long long c = 0;
       for (int rep = 0; rep < 2; rep++) {
         hipLaunchKernelGGL(ks[v], dim3(256), dim3(256 * w), 0, 0, in, out, iters, cyc);
