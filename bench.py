@@ -220,9 +220,13 @@ def cpu_baseline_all_cores(traces_dev, outcome_dev, mode, seconds):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
+    granted = oracle.cpu_cores_granted(threads)
+    mem = {f"{t}_threads": round(oracle.host_read_gbps(t, host), 1) for t in (1, threads)}
     return {"value": round(done / el, 1), "unit": "traces/s", "cores": threads, "kind": "port",
+            "cores_granted": round(granted, 2), "host_read_GBps": mem,
             "sample": f"{sample_n} traces, oracle/kbz_oracle.c kbzo_triage_batch_mt, "
-                      f"{threads} threads (sched_getaffinity, cgroup quota)"}
+                      f"{threads} threads (sched_getaffinity, cgroup quota); cores_granted = "
+                      f"threads x t(1) / t(threads) of a register-only chain per thread"}
 
 
 # ---- roofline traffic (PMC) --------------------------------------------------------------------

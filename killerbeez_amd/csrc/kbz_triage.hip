@@ -1799,6 +1799,9 @@ constexpr int kWideNX = KBZ_WIDE_NX;        // transform waves of k_pass1w
 constexpr int kWideNL = KBZ_WIDE_NL;        // loader waves of k_pass1w
 constexpr int kWideD = KBZ_WIDE_D;          // their register ring depth
 constexpr uint32_t kWideBelowChunks = 512;  // 2 chunks per CU on a 256-CU MI355X
+#ifndef KBZ_EVENT_SCOPE  // timing-only A/B builds: 0 = default (system-scope) event fences
+#define KBZ_EVENT_SCOPE hipEventReleaseToDevice
+#endif
 #ifndef KBZ_PASS1_DEPTH
 #define KBZ_PASS1_DEPTH 2
 #endif
@@ -2080,8 +2083,10 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
   if (c->timing) {
     if (c->ev_used_n == c->ev_pass1.size()) {
       std::pair<hipEvent_t, hipEvent_t> e;
-      HIP_TRY(hipEventCreate(&e.first));
-      HIP_TRY(hipEventCreate(&e.second));
+      // device-scope release: the default system-scope fence adds ~13 us per batch on MI355X
+      // (same-box A/B, profiles/r02_v9)
+      HIP_TRY(hipEventCreateWithFlags(&e.first, KBZ_EVENT_SCOPE));
+      HIP_TRY(hipEventCreateWithFlags(&e.second, KBZ_EVENT_SCOPE));
       c->ev_pass1.push_back(e);
     }
     ev = &c->ev_pass1[c->ev_used_n++].first;

@@ -80,8 +80,20 @@ def lib():
         L.kbzo_triage_batch.argtypes = args
         L.kbzo_triage_batch_mt.restype = C.c_int
         L.kbzo_triage_batch_mt.argtypes = args + [C.c_int]
+        L.kbzo_cpu_probe.restype = C.c_double
+        L.kbzo_cpu_probe.argtypes = [C.c_int, C.c_long]
+        L.kbzo_mem_probe.restype = C.c_double
+        L.kbzo_mem_probe.argtypes = [C.c_int, C.c_void_p, C.c_size_t, C.c_int]
         _lib = L
     return _lib
+
+
+def cpu_cores_granted(threads: int, iters: int = 200_000_000) -> float:
+    """Cores this process actually gets with `threads` OpenMP threads: one register-only
+    chain per thread, threads x t(1) / t(threads)."""
+    t1 = lib().kbzo_cpu_probe(1, iters)
+    tn = lib().kbzo_cpu_probe(threads, iters)
+    return threads * t1 / tn if tn > 0 else 0.0
 
 
 def have_ref() -> bool:
@@ -200,3 +212,10 @@ def ipt_keys(events: np.ndarray, lib_starts=(), lib_ends=(), lib_hashes=(), targ
     n = f(_p(ev), ev.shape[0], ls.size, _p(ls), _p(le), _p(lh), int(target_start),
           int(target_end), _p(out))
     return out[:n]
+
+
+def host_read_gbps(threads: int, buf: np.ndarray, passes: int = 3) -> float:
+    """Host memory read bandwidth (GB/s) of `threads` threads streaming disjoint slices of buf."""
+    b = np.ascontiguousarray(buf).view(np.uint8).reshape(-1)
+    el = lib().kbzo_mem_probe(threads, _p(b), b.size, passes)
+    return passes * b.size / el / 1e9 if el > 0 else 0.0

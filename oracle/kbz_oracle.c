@@ -10,6 +10,7 @@
 
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -450,4 +451,49 @@ size_t kbzo_ipt_keys(const uint64_t *ev, size_t n_ev, size_t nlib, const uint64_
   free(tnt);
   free(tip);
   return execs;
+}
+
+/* CPU parallelism probe for bench.py's all-core baseline (not a restatement of anything): every
+ * one of `threads` OpenMP threads runs the same dependent hash32-step chain of `iters` steps
+ * (registers only, no memory traffic).  Returns the wall time in seconds; with T real cores the
+ * time equals the 1-thread time, so threads * t1 / tT is the number of cores actually granted. */
+double kbzo_cpu_probe(int threads, long iters) {
+  if (threads < 1) threads = 1;
+  volatile uint64_t sink = 0;
+  struct timespec a, b;
+  clock_gettime(CLOCK_MONOTONIC, &a);
+#pragma omp parallel num_threads(threads)
+  {
+    uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)(size_t)&h;
+    for (long i = 0; i < iters; i++) h = h32_step(h, (uint64_t)i);
+    sink += h;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &b);
+  (void)sink;
+  return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}
+
+/* Host memory-stream probe for the same baseline: `threads` threads each read their own slice of
+ * `buf` (n bytes, 8-byte words) `passes` times.  Returns wall seconds; bytes read = passes * n. */
+double kbzo_mem_probe(int threads, const uint8_t *buf, size_t n, int passes) {
+  if (threads < 1) threads = 1;
+  volatile uint64_t sink = 0;
+  struct timespec a, b;
+  clock_gettime(CLOCK_MONOTONIC, &a);
+#pragma omp parallel num_threads(threads)
+  {
+#ifdef _OPENMP
+    const int t = omp_get_thread_num();
+#else
+    const int t = 0;
+#endif
+    const size_t words = n / 8, lo = words * (size_t)t / threads, hi = words * (size_t)(t + 1) / threads;
+    uint64_t acc = 0;
+    for (int p = 0; p < passes; p++)
+      for (size_t i = lo; i < hi; i++) acc += ld64(buf + 8 * i);
+    sink += acc;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &b);
+  (void)sink;
+  return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
 }

@@ -50,6 +50,13 @@ int kbzo_triage_batch_mt(int mode, const uint8_t *traces, size_t n, size_t strid
                          const uint8_t *ignore, uint32_t *last_hash, int want,
                          uint8_t *hnb_out, uint32_t *h32_out, uint64_t *x64_out, int threads);
 
+/* bench.py's all-core baseline: wall seconds for `threads` threads each running an
+ * `iters`-step register-only hash chain (t1 / tT x threads = cores actually granted). */
+double kbzo_cpu_probe(int threads, long iters);
+/* ... and a host memory-stream probe: `threads` threads read disjoint slices of buf (n bytes)
+ * `passes` times; returns wall seconds. */
+double kbzo_mem_probe(int threads, const uint8_t *buf, size_t n, int passes);
+
 /* Merger fold (merger/merger.c:79-99): dest = AND of n states, each `state_bytes` long. */
 void kbzo_merge_many(uint8_t *dest, const uint8_t *states, size_t n, size_t state_bytes);
 
