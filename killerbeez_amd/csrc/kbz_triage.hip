@@ -1208,6 +1208,10 @@ __global__ __launch_bounds__(256) void k_total(uint8_t *segor, uint32_t nseg, in
   *(uint64_t *)(total + (size_t)k * map_size + col) = acc;
 }
 
+#ifndef KBZ_SCAN_ILP  // chunk rows k_scan loads per round trip: 8 beat 16 and 32 on fresh config-2
+                      // batches (step 0.77-0.78 vs 0.80-0.81 ms, profiles/r02_v10/ab_scan_ilp.txt)
+#define KBZ_SCAN_ILP 8
+#endif
 // item: [7:0] new bits, [8] score-2 candidate, [10:9] class, [34:11] column, [63:35] chunk
 __device__ __forceinline__ uint64_t pack_item(uint32_t chunk, int k, uint32_t col, uint32_t nb,
                                               bool f2) {
@@ -1341,7 +1345,8 @@ __global__ __launch_bounds__(256) void k_scan(const uint8_t *chunk_or, const uin
   // Only chunks that hold traces of class k AND stored (or, DynamoRIO fix path, recomputed) one
   // of this wave's 4 tiles can add bits here: an unstored tile held no still-virgin bit, so a
   // skipped chunk changes neither the claims nor the running OR.  Lane l tests chunk cg + l;
-  // the wave walks the set bits of the ballot in order, 8 chunk loads per memory round trip.
+  // the wave walks the set bits of the ballot in order, KBZ_SCAN_ILP chunk loads per memory round
+  // trip.
   const uint32_t t0 = (blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * 16 / kTileW;
   for (uint32_t cg = c0; cg < c1; cg += 64) {
     const uint32_t cl = cg + (threadIdx.x & 63);
@@ -1351,23 +1356,23 @@ __global__ __launch_bounds__(256) void k_scan(const uint8_t *chunk_or, const uin
             ((tflags[((size_t)cl * nclass + k) * nfw + (t0 >> 6)] >> (t0 & 63)) & 0xFull);
     uint64_t mask = __ballot(any);
     while (mask) {
-      uint32_t cs[8];
+      uint32_t cs[KBZ_SCAN_ILP];
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < KBZ_SCAN_ILP; u++) {
         cs[u] = mask ? cg + (uint32_t)__builtin_ctzll(mask) : ~0u;
         mask &= mask - 1;
       }
-      uint4 o[8];
-      bool st[8];
+      uint4 o[KBZ_SCAN_ILP];
+      bool st[KBZ_SCAN_ILP];
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < KBZ_SCAN_ILP; u++) {
         const uint32_t c = cs[u] != ~0u ? cs[u] : cs[0];
         o[u] = *(const uint4 *)(chunk_or + (size_t)c * nclass * map_size + kc);
         // DynamoRIO fix path: a listed chunk's row was rewritten whole (unmasked) by k_total
         st[u] = tile_stored(tflags, nfw, nclass, c, k, col) || (listed && listed[c]);
       }
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < KBZ_SCAN_ILP; u++) {
         const uint32_t c = cs[u];  // uniform across the wave
         if (c == ~0u) break;
         if (!st[u]) o[u] = make_uint4(0, 0, 0, 0);  // nothing still virgin in that tile

@@ -214,6 +214,31 @@ static void apply_xform(uint8_t *t, size_t m, int xf) {
   else if (xf == XF_SIMPLIFY) kbzo_simplify_trace(t, m);
 }
 
+/* The same transforms, word at a time with a byte table (the multi-threaded path below; its
+ * results are pinned to the byte loops above by tests/test_oracle_pin.py).  dst may be src. */
+static uint8_t g_cls_lut[256];
+static void init_lut(void) {
+  for (int c = 0; c < 256; c++) g_cls_lut[c] = kbzo_count_class((uint8_t)c);
+}
+static void xform_words(uint8_t *dst, const uint8_t *src, size_t m, int xf) {
+  for (size_t w = 0; w < m; w += 8) {
+    uint64_t v = ld64(src + w);
+    if (xf == XF_SIMPLIFY) {
+      uint64_t r = 0;
+      for (int b = 0; b < 8; b++) r |= (uint64_t)(((v >> (8 * b)) & 0xff) ? 0x80 : 0x01) << (8 * b);
+      v = r;
+    } else if (xf == XF_CLASSIFY && v) {
+      uint64_t r = 0;
+      for (int b = 0; b < 8; b++) r |= (uint64_t)g_cls_lut[(v >> (8 * b)) & 0xff] << (8 * b);
+      v = r;
+    }
+    st64(dst + w, v);
+  }
+}
+static void or_words(uint8_t *acc, const uint8_t *x, size_t m) {
+  for (size_t w = 0; w < m; w += 8) st64(acc + w, ld64(acc + w) | ld64(x + w));
+}
+
 static int check_args(int mode, size_t stride, size_t map_size) {
   if (mode < 0 || mode > 2) return -1;
   if (map_size == 0 || (map_size & 7) || stride < map_size) return -1;
@@ -289,6 +314,7 @@ int kbzo_triage_batch_mt(int mode, const uint8_t *traces, size_t n, size_t strid
     return -1;
   }
   const uint32_t seed = 0xa5b35705u;
+  init_lut();
 #pragma omp parallel num_threads(threads)
   {
 #ifdef _OPENMP
@@ -301,15 +327,13 @@ int kbzo_triage_batch_mt(int mode, const uint8_t *traces, size_t n, size_t strid
     for (size_t j = lo; j < hi; j++) {
       int oc = outcome ? outcome[j] : KBZO_FUZZ_NONE;
       uint8_t *x = (j == lo) ? first + (size_t)s * m : t;
-      memcpy(x, traces + j * stride, m);
-      apply_xform(x, m, trace_xform(mode, oc));
+      xform_words(x, traces + j * stride, m, trace_xform(mode, oc));
       h[j] = ignore ? kbzo_hash32_with_ignore(x, ignore, (uint32_t)m, seed)
                     : kbzo_hash32(x, (uint32_t)m, seed);
       if (x64_out && (want & KBZO_WANT_X64)) x64_out[j] = kbzo_xxh64(x, m, 0);
       if (j == lo) continue;
       if (dr && (skip[j] = h[j] == h[j - 1])) continue;
-      uint8_t *a = aggr + ((size_t)s * nmaps + trace_map(mode, oc)) * m;
-      for (size_t i = 0; i < m; i++) a[i] |= x[i];
+      or_words(aggr + ((size_t)s * nmaps + trace_map(mode, oc)) * m, x, m);
     }
     free(t);
   }
@@ -349,8 +373,7 @@ int kbzo_triage_batch_mt(int mode, const uint8_t *traces, size_t n, size_t strid
       int oc = outcome ? outcome[j] : KBZO_FUZZ_NONE;
       uint8_t r = 0;
       if (!skip[j]) {
-        memcpy(t, traces + j * stride, m);
-        apply_xform(t, m, trace_xform(mode, oc));
+        xform_words(t, traces + j * stride, m, trace_xform(mode, oc));
         uint8_t *v = entry + ((size_t)s * nmaps + trace_map(mode, oc)) * m;
         r = ignore ? kbzo_has_new_bits_with_ignore(t, v, ignore, m) : kbzo_has_new_bits(v, t, m);
       }
