@@ -347,10 +347,12 @@ def main_triage(args):
     fresh = pool[args.warmup:] if npool > args.warmup else pool
     elapsed, pass1_ms = timed(fresh, args.steps)
     n_fresh = min(args.steps, len(fresh))
+    fresh_stats = ctx.stats()  # work of the last timed batch (claim items resolved, ...)
     value = world * B * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
     achieved = B * M / (pass1_ms * 1e-3) / 1e9  # GB/s, algorithmic bytes of one launch
-    variants = {"cold_first_batch_ms": round(cold_ms, 4)}
+    variants = {"cold_first_batch_ms": round(cold_ms, 4),
+                "last_fresh_batch_work": fresh_stats}
     if not args.no_variants:
         seen = pool[-2:]
         el2, p2 = timed(seen, args.steps)
