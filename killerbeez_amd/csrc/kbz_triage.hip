@@ -240,6 +240,9 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #ifndef KBZ_WIDE_LPRIO
 #define KBZ_WIDE_LPRIO 3
 #endif
+#ifndef KBZ_WIDE_PEEL  // k_pass1w transform waves: steady steps without bounds tests
+#define KBZ_WIDE_PEEL 1
+#endif
 #ifndef KBZ_WIDE_BAL
 #define KBZ_WIDE_BAL 1
 #endif
@@ -864,7 +867,8 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
       }
 #pragma unroll
       for (int k = 0; k < NC; k++)
-        if (present[k] && ow[k]) atomicOr((unsigned long long *)&orb[b][k][w], (unsigned long long)ow[k]);
+        if (present[k] && (KBZ_WIDE_PEEL || ow[k]))  // (dense maps: a zero OR is rare)
+          atomicOr((unsigned long long *)&orb[b][k][w], (unsigned long long)ow[k]);
     };
     // X_0: the virgin words of tile t, loaded into vpre[t & 1] at the end of step t+1, two
     // steps before finish_tile(t) needs them
@@ -917,32 +921,46 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
       }
     };
     KBZ_STAMP_DECL;
-    auto step = [&](uint32_t s, auto pc) {
+    auto step = [&](uint32_t s, auto pc, auto stc) {
       constexpr int p = decltype(pc)::value;  // s & 1
+      constexpr bool ST = decltype(stc)::value;  // 3 <= s <= ntiles: every part runs (no tests)
       // (1) LDS reads, issued first and waited for only after the transform (the LDS queue is
       // long right after the barrier, with every wave's fills, reads and writes): the previous
       // group's last row of tile s-3, then the words of tile s-1 (transformed next step)
       uint64_t pl = 0;
-      const bool fin = s >= 3 && s - 3 < ntiles;
+      const bool fin = ST || (s >= 3 && s - 3 < ntiles);
+      const bool rd = ST || (s >= 1 && s - 1 < ntiles);
       if (MODE == KBZ_MODE_DYNAMORIO && fin && grp > 0) pl = bnd[p ^ 1][grp - 1][w];
-      if (s >= 1 && s - 1 < ntiles) read_tile(s - 1, IntC<p ^ 1>{});
+      if (rd) read_tile(s - 1, IntC<p ^ 1>{});
       const uint64_t fw = ftw, fr = frel;  // tile s-3's, from its transform at step s-1
       KBZ_STAMP(2);
       // (2) transform tile s-2 from the registers read at step s-1
-      if (s >= 2 && s - 2 < ntiles) transform_tile(s - 2, IntC<p>{});
+      if (ST || (s >= 2 && s - 2 < ntiles)) transform_tile(s - 2, IntC<p>{});
       KBZ_STAMP(0);
       // (3) finish tile s-3
       if (fin) finish_tile(s - 3, pl, fw, fr, IntC<p ^ 1>{});
       // (4) X_0: virgin words of tile s-1 (finished at step s+2; vpre[p ^ 1] was last read by
       // finish_tile(s-3) above)
-      if (xi == 0 && s >= 1 && s - 1 < ntiles) load_virgin(s - 1, IntC<p ^ 1>{});
+      if (xi == 0 && rd) load_virgin(s - 1, IntC<p ^ 1>{});
       KBZ_STAMP(3);
       lds_barrier_seen();
       KBZ_STAMP(1);
     };
-    for (uint32_t s0 = 0; s0 < nb; s0 += 2) {
-      step(s0, IntC<0>{});
-      if (s0 + 1 < nb) step(s0 + 1, IntC<1>{});
+    uint32_t s0 = 0;
+#if KBZ_WIDE_PEEL
+    // steps 0-3 and the last ones test which parts run; the steady steps in between do not
+    for (; s0 < 4 && s0 < nb; s0 += 2) {
+      step(s0, IntC<0>{}, IntC<0>{});
+      if (s0 + 1 < nb) step(s0 + 1, IntC<1>{}, IntC<0>{});
+    }
+    for (; s0 + 1 <= ntiles; s0 += 2) {
+      step(s0, IntC<0>{}, IntC<1>{});
+      step(s0 + 1, IntC<1>{}, IntC<1>{});
+    }
+#endif
+    for (; s0 < nb; s0 += 2) {
+      step(s0, IntC<0>{}, IntC<0>{});
+      if (s0 + 1 < nb) step(s0 + 1, IntC<1>{}, IntC<0>{});
     }
     KBZ_STAMP_FLUSH(chunk * 16 + wave);
     uint64_t nm = 0;  // rows that differ from their predecessor
