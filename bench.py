@@ -95,6 +95,12 @@ def maybe_launch(args):
         sys.exit(subprocess.call(cmd, env=env))
 
 
+# Rehearsal of the multi-rank path on a one-GPU box (never for reported numbers): with
+# KBZ_BENCH_REHEARSE=1 every rank uses cuda:0 and the collectives go through gloo (RCCL needs
+# one GPU per rank).
+REHEARSE = os.environ.get("KBZ_BENCH_REHEARSE") == "1"
+
+
 def init_dist():
     import torch
     import torch.distributed as dist
@@ -102,10 +108,13 @@ def init_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", local if world > 1 and not REHEARSE else 0)
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if REHEARSE:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     return world, rank, dev
 
 
@@ -115,7 +124,10 @@ def barrier_sync(world, dev):
 
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier(device_ids=[dev.index])
+        if REHEARSE:
+            dist.barrier()
+        else:
+            dist.barrier(device_ids=[dev.index])
     torch.cuda.synchronize()
 
 
