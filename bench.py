@@ -59,8 +59,9 @@ def parse():
     p.add_argument("--no-variants", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--pmc", action="store_true",
-                   help="measure roofline.traffic live: two rocprofv3 --pmc passes of a child run")
+    p.add_argument("--no-pmc", dest="pmc", action="store_false",
+                   help="skip the live roofline.traffic measurement (two rocprofv3 --pmc passes "
+                        "of a short child run, rank 0 with 1 GPU) and report the stored one")
     p.add_argument("--seed", type=int, default=0x5EED)
     p.add_argument("--workload", default="config2",
                    choices=["config2", "config3", "merge", "stream", "plugin"])
@@ -243,7 +244,7 @@ def cpu_baseline_all_cores(traces_dev, outcome_dev, mode, seconds):
 
 # ---- roofline traffic (PMC) --------------------------------------------------------------------
 
-def _pmc_pass(counter, workload_args, outdir, timeout=240):
+def _pmc_pass(counter, workload_args, outdir, timeout=150):
     """One rocprofv3 --pmc pass over a short child run; per-dispatch values of `counter` for
     the pass-1 kernel, in launch order."""
     import csv
@@ -251,7 +252,7 @@ def _pmc_pass(counter, workload_args, outdir, timeout=240):
 
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir, "-o", "run",
            "--", sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-variants",
-           *workload_args]
+           "--no-pmc", *workload_args]
     subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=timeout,
                    check=True)
     vals = []
@@ -388,6 +389,7 @@ def main_triage(args):
                 "what": f"{len(rb)} of the fresh batches with {args.repeat_frac:.0%} of execs "
                         "repeating their predecessor (last-hash skips), virgin carried"}
     del pool, fresh
+    torch.cuda.empty_cache()  # the PMC child run below allocates its own batches
     traffic = None
     if rank == 0 and world == 1 and args.pmc:
         try:

@@ -26,21 +26,21 @@ for s in $STEPS; do
     prof)
       echo "== rocprofv3 $(date +%T)"
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run \
-        -- python3 bench.py --steps 40 --warmup 2 --no-cpu ${BENCH_ARGS:-} > $OUT/prof.log 2>&1
+        -- python3 bench.py --steps 40 --warmup 2 --no-cpu --no-pmc ${BENCH_ARGS:-} > $OUT/prof.log 2>&1
       rc=$?; tail -3 $OUT/prof.log; [ $rc -eq 0 ] || exit $rc
       find $OUT/prof -name "*stats*.csv" | head -5 ;;
     pmc)
       echo "== rocprofv3 pmc $(date +%T)"
       timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc1 -o run \
-        -- python3 bench.py --steps 3 --warmup 1 --no-cpu ${BENCH_ARGS:-} > $OUT/pmc1.log 2>&1
+        -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-pmc ${BENCH_ARGS:-} > $OUT/pmc1.log 2>&1
       rc=$?; tail -2 $OUT/pmc1.log; [ $rc -eq 0 ] || exit $rc
       timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc2 -o run \
-        -- python3 bench.py --steps 3 --warmup 1 --no-cpu ${BENCH_ARGS:-} > $OUT/pmc2.log 2>&1
+        -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-pmc ${BENCH_ARGS:-} > $OUT/pmc2.log 2>&1
       rc=$?; tail -2 $OUT/pmc2.log; [ $rc -eq 0 ] || exit $rc ;;
     sq)
       echo "== rocprofv3 SQ counters $(date +%T)"
       timeout -k 10 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
-        --output-format csv -d $OUT/sq -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ${BENCH_ARGS:-} > $OUT/sq.log 2>&1
+        --output-format csv -d $OUT/sq -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-pmc ${BENCH_ARGS:-} > $OUT/sq.log 2>&1
       rc=$?; tail -2 $OUT/sq.log; [ $rc -eq 0 ] || exit $rc ;;
     probe)
       echo "== bwprobe $(date +%T)"

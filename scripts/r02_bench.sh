@@ -22,8 +22,8 @@ for s in ${STEPS:-bench plugin merge stream prof pmc}; do
     stream) run stream 300 python bench.py --workload stream --steps 40 ;;
     config3) run config3 600 python bench.py --workload config3 --steps 10 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run \
-              -- python3 bench.py --no-cpu ;;
-    pmc)    run pmc 600 python bench.py --pmc --no-cpu --no-variants --steps 10 ;;
+              -- python3 bench.py --no-cpu --no-pmc ;;
+    pmc)    run pmc 600 python bench.py --no-cpu --no-variants --steps 10 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
