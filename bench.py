@@ -302,6 +302,36 @@ def stored_traffic(workload):
 
 # ---- triage workloads (config 2 / config 3) ----------------------------------------------------
 
+def crash_variant(args, pool, barrier_sync, dev, steps=5):
+    """SURVEY.md §8(d) 'simplify-mode (crash) variant': the same traces triaged in AFL mode with
+    every exec a crash (finish_fuzz_round, afl_instrumentation.c:260-265: simplify_trace, then
+    has_new_bits against virgin_crash), on a context of its own."""
+    import torch
+
+    from killerbeez_amd.triage import MODES, WANT_H32, TriageContext
+
+    B, M = args.batch, args.map_size
+    crash = torch.full((B,), 2, dtype=torch.int8, device=dev)  # KBZ_FUZZ_CRASH
+    with TriageContext(M, MODES["afl"], B) as c2:
+        out = {"hnb": torch.empty(B, dtype=torch.uint8, device=dev),
+               "h32": torch.empty(B, dtype=torch.int32, device=dev)}
+        c2.triage(pool[0][0], crash, WANT_H32, out=out)  # warmup
+        barrier_sync(1, dev)
+        c2.sync()
+        c2.time_pass1(True)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            c2.triage(pool[(i + 1) % len(pool)][0], crash, WANT_H32, out=out)
+        barrier_sync(1, dev)
+        el = time.perf_counter() - t0
+        ms, launches = c2.time_pass1(False)
+        c2.sync()
+    return {"value": round(B * steps / el, 1), "ms_per_step": round(1e3 * el / steps, 4),
+            "pass1_ms": round(ms / max(1, launches), 4),
+            "what": f"{steps} batches of the pool in AFL mode, every exec a crash (simplify + "
+                    "virgin_crash), own context"}
+
+
 def main_triage(args):
     import torch
 
@@ -388,6 +418,8 @@ def main_triage(args):
                 "repeated_execs": reps, "last_batch_fixed_chunks": st["fixed_chunks"],
                 "what": f"{len(rb)} of the fresh batches with {args.repeat_frac:.0%} of execs "
                         "repeating their predecessor (last-hash skips), virgin carried"}
+        if world == 1:
+            variants["afl_all_crash_simplify"] = crash_variant(args, pool, barrier_sync, dev)
     del pool, fresh
     torch.cuda.empty_cache()  # the PMC child run below allocates its own batches
     traffic = None

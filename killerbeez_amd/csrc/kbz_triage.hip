@@ -240,6 +240,9 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #ifndef KBZ_WIDE_LPRIO
 #define KBZ_WIDE_LPRIO 3
 #endif
+#ifndef KBZ_PASS1_TMIX  // timing variants: 0 = wave L mixes in every mode
+#define KBZ_PASS1_TMIX 1
+#endif
 #ifndef KBZ_WIDE_PEEL  // k_pass1w transform waves: steady steps without bounds tests
 #define KBZ_WIDE_PEEL 1
 #endif
@@ -293,6 +296,11 @@ struct Pass1Args {
 template <int MODE, bool IGN, bool X64, int ABL = 0, int D = 4>
 __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
+  // AFL mode: wave T also computes the hash32 mix of every word it transforms and leaves it in
+  // LDS for wave L (T only simplifies the few hang/crash rows there, L was the slower wave:
+  // pass 1 1.23 -> 1.13 ms, profiles/r02_v18).  DynamoRIO and AFL_CLASSIFY keep the mix on L:
+  // T's classify makes T the busier wave there.  XXH64 needs the transformed words on L.
+  constexpr bool TMIX = KBZ_PASS1_TMIX && MODE == KBZ_MODE_AFL && !X64;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = 8;  // 8 x 1-KiB loads per wave per tile
   constexpr int TILE = kChunk * SLOTS;                     // uint4 per tile buffer
   // 2 tile buffers (32 KiB) + 8 KiB: wave T's virgin words (2 x 768 B) and padding, at most 4
@@ -367,7 +375,10 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
             const int wi = 2 * (q + qq) + e;
             const uint64_t w = ld_u64(v, e);
             uint64_t tw, k;
-            if (__ballot(w != 0)) {
+            if (TMIX) {  // wave T left the word's hash32 mix (0 only for a raw 0 word)
+              tw = 0;
+              k = (simp && w == 0) ? ksimp : w;
+            } else if (__ballot(w != 0)) {
               tw = (simp && w == 0) ? kSimpleZero : w;
               k = h32_mix(tw & (IGN ? ig[wi] : ~0ull));
             } else {
@@ -488,8 +499,9 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
           const uint64_t x = ld_u64(v, e);
           if (__ballot(x != 0)) {
             const uint64_t tw = xform8(x, xf);
-            if (e) { v.z = (uint32_t)tw; v.w = (uint32_t)(tw >> 32); }
-            else { v.x = (uint32_t)tw; v.y = (uint32_t)(tw >> 32); }
+            const uint64_t out = TMIX ? h32_mix(tw) : tw;  // what wave L chains next step
+            if (e) { v.z = (uint32_t)out; v.w = (uint32_t)(out >> 32); }
+            else { v.x = (uint32_t)out; v.y = (uint32_t)(out >> 32); }
             dirty = true;
 #pragma unroll
             for (int k = 0; k < NC; k++) {
@@ -508,8 +520,8 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
               if (present[k]) orw[k] = (lane == wi) ? kSimpleZero : orw[k];
           }
         }
-        // raw AFL words are their own transform (only simplified lanes change)
-        if (dirty && (MODE != KBZ_MODE_AFL || simp)) *slot = v;
+        // raw AFL words are their own transform (only simplified lanes change) unless T mixes
+        if (dirty && (TMIX || MODE != KBZ_MODE_AFL || simp)) *slot = v;
       }
       // chunk_or keeps only bits still virgin at batch entry (orw & V): the scan uses nothing
       // else (its new bits are o & V & ~prev, and f2 only looks at bytes with V == 0xff), and a
