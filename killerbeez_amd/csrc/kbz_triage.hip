@@ -240,6 +240,12 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #ifndef KBZ_WIDE_LPRIO
 #define KBZ_WIDE_LPRIO 3
 #endif
+#ifndef KBZ_PASS1_SROWS  // timing variants: 0 = per-word reductions for every class
+#define KBZ_PASS1_SROWS 1
+#endif
+#ifndef KBZ_SROWS_MAX
+#define KBZ_SROWS_MAX 8
+#endif
 #ifndef KBZ_PASS1_TMIX  // timing variants: 0 = wave L mixes in every mode
 #define KBZ_PASS1_TMIX 1
 #endif
@@ -301,6 +307,8 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   // pass 1 1.23 -> 1.13 ms, profiles/r02_v18).  DynamoRIO and AFL_CLASSIFY keep the mix on L:
   // T's classify makes T the busier wave there.  XXH64 needs the transformed words on L.
   constexpr bool TMIX = KBZ_PASS1_TMIX && MODE == KBZ_MODE_AFL && !X64;
+  // AFL modes: the simplified classes' column ORs come from their rows, once per tile
+  constexpr bool SROWS = KBZ_PASS1_SROWS && NC > 1;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = 8;  // 8 x 1-KiB loads per wave per tile
   constexpr int TILE = kChunk * SLOTS;                     // uint4 per tile buffer
   // 2 tile buffers (32 KiB) + 8 KiB: wave T's virgin words (2 x 768 B) and padding, at most 4
@@ -444,8 +452,14 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   } else {
     // ------------------------------------------------------------------ wave T
     uint64_t present[NC];
+    // every simplified class has at most KBZ_SROWS_MAX rows in this chunk: their column ORs
+    // come from their rows, once per tile (wave-uniform; crash-heavy chunks take the other path)
+    bool rowwise = SROWS;
 #pragma unroll
-    for (int k = 0; k < NC; k++) present[k] = __ballot(valid && cls == k);
+    for (int k = 0; k < NC; k++) {
+      present[k] = __ballot(valid && cls == k);
+      if (k > 0 && __popcll(present[k]) > KBZ_SROWS_MAX) rowwise = false;
+    }
     if (lane == 0) {
       uint8_t m = 0;
 #pragma unroll
@@ -478,12 +492,31 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
 #pragma unroll
     for (int k = 0; k < NC; k++) tfl[k] = 0;
     uint64_t *tfbase = a.tflags + (size_t)chunk * NC * a.nfw;
-    auto transform_tile = [&](uint32_t s) {
+    auto transform_tile = [&](uint32_t s, auto rwc) {
+      constexpr bool RW = decltype(rwc)::value;  // simplified classes ORed row-wise (few rows)
       const int b = s & 1;
       const uint64_t *ig = IGN ? (const uint64_t *)(a.ignore + (size_t)s * TW) : nullptr;
       uint64_t orw[NC];
 #pragma unroll
       for (int k = 0; k < NC; k++) orw[k] = 0;
+      if (RW) {
+        // hang / crash classes with few rows in the chunk (the usual case: 2 % of execs): OR their
+        // raw rows word-parallel (lane = word), before the word loop rewrites the tile in place --
+        // instead of a 64-lane reduction per class for every nonzero word (AFL pass 1 1.15 ->
+        // 0.80 ms, profiles/r02_v19).  simplify8(0) = 0x01 bytes covers words that are zero in
+        // every row.  Crash-heavy chunks keep the per-word reductions.
+        const uint64_t *tile = (const uint64_t *)&lds[b * TILE];
+        const int wl = lane & 31;  // lanes 32-63 duplicate 0-31 (only lanes < 32 are stored)
+#pragma unroll
+        for (int k = 1; k < NC; k++) {
+          uint64_t acc = 0;
+          for (uint64_t mm = present[k]; mm; mm &= mm - 1) {
+            const int rr = __builtin_ctzll(mm);  // wave-uniform
+            acc |= simplify8(tile[(rr * SLOTS + ((wl >> 1) ^ (rr & 15))) * 2 + (wl & 1)]);
+          }
+          orw[k] = acc;
+        }
+      }
       uint4 *row = &lds[b * TILE + lane * SLOTS];
       const int sw = lane & 15;
       uint4 vnext = row[0 ^ sw];
@@ -504,7 +537,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
             else { v.x = (uint32_t)out; v.y = (uint32_t)(out >> 32); }
             dirty = true;
 #pragma unroll
-            for (int k = 0; k < NC; k++) {
+            for (int k = 0; k < (RW ? 1 : NC); k++) {
               if (present[k]) {
                 const uint64_t r = wave_or64((valid && cls == k) ? tw : 0);
                 orw[k] = (lane == wi) ? r : orw[k];
@@ -514,7 +547,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
               const uint64_t rel = IGN ? ~nonzero_bytes8(ig[wi]) : ~0ull;
               neq |= (tw ^ from_prev_lane(tw)) & rel;
             }
-          } else if (MODE != KBZ_MODE_DYNAMORIO) {
+          } else if (MODE != KBZ_MODE_DYNAMORIO && !RW) {
 #pragma unroll
             for (int k = 1; k < NC; k++)  // simplified classes see 0x01 bytes everywhere
               if (present[k]) orw[k] = (lane == wi) ? kSimpleZero : orw[k];
@@ -561,7 +594,10 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         store_t(R[u], s & 1);
         load_t(R[u], s + D);
         KBZ_STAMP(2);
-        if (s < ntiles) transform_tile(s);
+        if (s < ntiles) {
+          if (SROWS && rowwise) transform_tile(s, IntC<1>{});
+          else transform_tile(s, IntC<0>{});
+        }
         KBZ_STAMP(0);
         lds_barrier();
         KBZ_STAMP(3);
