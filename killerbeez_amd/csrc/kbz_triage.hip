@@ -244,7 +244,7 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #define KBZ_PASS1_SROWS 1
 #endif
 #ifndef KBZ_SROWS_MAX
-#define KBZ_SROWS_MAX 8
+#define KBZ_SROWS_MAX 16  // 8, 16, 32 equal at 2 % hangs + crashes; 4 is slower (profiles/r02_v19)
 #endif
 #ifndef KBZ_PASS1_TMIX  // timing variants: 0 = wave L mixes in every mode
 #define KBZ_PASS1_TMIX 1
