@@ -235,7 +235,7 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #define KBZ_WIDE_NL 4
 #endif
 #ifndef KBZ_WIDE_D
-#define KBZ_WIDE_D 2
+#define KBZ_WIDE_D 3  // 3 vs 2: config 3 pass 1 3.75-3.77 vs 3.81-3.86 ms same-box (profiles/r02_final2)
 #endif
 #ifndef KBZ_WIDE_LPRIO
 #define KBZ_WIDE_LPRIO 3
