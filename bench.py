@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--pool", type=int, default=0,
                    help="distinct batches (default warmup + steps, capped by free HBM)")
     p.add_argument("--repeat-frac", type=float, default=0.9)
+    p.add_argument("--hash", action="store_true",
+                   help="AFL modes: also compute hash32 (the reference AFL plugin never hashes, "
+                        "afl_instrumentation.c:231-274; DynamoRIO mode always does)")
     p.add_argument("--no-variants", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
@@ -272,7 +275,7 @@ def live_traffic(args, warmup=1, steps=4):
 
     wa = ["--workload", args.workload, "--mode", args.mode, "--batch", str(args.batch),
           "--map-size", str(args.map_size), "--warmup", str(warmup), "--steps", str(steps),
-          "--seed", str(args.seed)]
+          "--seed", str(args.seed), *(["--hash"] if args.hash else [])]
     with tempfile.TemporaryDirectory() as d:
         fetch = _pmc_pass("FETCH_SIZE", wa, os.path.join(d, "f"))[warmup:]
         write = _pmc_pass("WRITE_SIZE", wa, os.path.join(d, "w"))[warmup:]
@@ -311,17 +314,19 @@ def crash_variant(args, pool, barrier_sync, dev, steps=5):
     from killerbeez_amd.triage import MODES, WANT_H32, TriageContext
 
     B, M = args.batch, args.map_size
+    want = WANT_H32 if args.hash else 0  # the reference AFL plugin never hashes
     crash = torch.full((B,), 2, dtype=torch.int8, device=dev)  # KBZ_FUZZ_CRASH
     with TriageContext(M, MODES["afl"], B) as c2:
-        out = {"hnb": torch.empty(B, dtype=torch.uint8, device=dev),
-               "h32": torch.empty(B, dtype=torch.int32, device=dev)}
-        c2.triage(pool[0][0], crash, WANT_H32, out=out)  # warmup
+        out = {"hnb": torch.empty(B, dtype=torch.uint8, device=dev)}
+        if want:
+            out["h32"] = torch.empty(B, dtype=torch.int32, device=dev)
+        c2.triage(pool[0][0], crash, want, out=out)  # warmup
         barrier_sync(1, dev)
         c2.sync()
         c2.time_pass1(True)
         t0 = time.perf_counter()
         for i in range(steps):
-            c2.triage(pool[(i + 1) % len(pool)][0], crash, WANT_H32, out=out)
+            c2.triage(pool[(i + 1) % len(pool)][0], crash, want, out=out)
         barrier_sync(1, dev)
         el = time.perf_counter() - t0
         ms, launches = c2.time_pass1(False)
@@ -329,7 +334,7 @@ def crash_variant(args, pool, barrier_sync, dev, steps=5):
     return {"value": round(B * steps / el, 1), "ms_per_step": round(1e3 * el / steps, 4),
             "pass1_ms": round(ms / max(1, launches), 4),
             "what": f"{steps} batches of the pool in AFL mode, every exec a crash (simplify + "
-                    "virgin_crash), own context"}
+                    f"virgin_crash), own context, {'with' if want else 'no'} hash32"}
 
 
 def main_triage(args):
@@ -351,18 +356,21 @@ def main_triage(args):
     pool = [gen(B, M, seed=args.seed + 7919 * p + 104729 * rank, device=dev, hot_seed=args.seed)
             for p in range(npool)]
     ctx = TriageContext(M, mode, B)
-    out = {"hnb": torch.empty(B, dtype=torch.uint8, device=dev),
-           "h32": torch.empty(B, dtype=torch.int32, device=dev)}
+    # DynamoRIO always hashes (last-hash skip); the AFL plugin never does unless asked
+    want = WANT_H32 if (mode == MODES["dynamorio"] or args.hash) else 0
+    out = {"hnb": torch.empty(B, dtype=torch.uint8, device=dev)}
+    if want:
+        out["h32"] = torch.empty(B, dtype=torch.int32, device=dev)
     counts = [B] * world
 
     def step(t, oc):
         if world == 1:
-            ctx.shard_begin(t, oc, WANT_H32, out=out)
+            ctx.shard_begin(t, oc, want, out=out)
             ctx.shard_link(None, None, True, None, None)
             ctx.shard_reduce()
             ctx.shard_finish(None, None)  # single shard: its own aggregate is the total
         else:
-            triage_sharded(ctx, t, oc, counts, rank, world, WANT_H32, device=dev)
+            triage_sharded(ctx, t, oc, counts, rank, world, want, device=dev)
 
     def timed(batches, k, events=False):
         """k steps over batches[i % len], bracketed by barrier + synchronize; max over ranks.
@@ -446,14 +454,19 @@ def main_triage(args):
                 f"{n_fresh} distinct never-seen batches in the timed steps)",
         "config": {"workload": f"{args.workload}: {B} {'dense' if dense else 'sparse'} "
                                f"traces/GPU x {M} B map, {args.mode} "
-                               "classify+hash32+last-hash skip+has_new_bits, virgin carried, "
-                               "fresh batches",
+                               + ("classify+hash32+last-hash skip+has_new_bits"
+                                  if mode == MODES["dynamorio"] else
+                                  ("classify" if args.mode == "afl_classify" else "raw") +
+                                  "/simplify+has_new_bits vs 3 virgin maps" +
+                                  ("+hash32" if want else " (no hash, as the AFL plugin)")) +
+                               ", virgin carried, fresh batches",
                    "map_size": M, "batch_per_gpu": B, "global_batch": world * B,
                    "mode": args.mode, "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic["bytes"], "traffic_source": traffic["source"],
-                     "kernel": "k_pass1s" if B >= 512 * 64 else "k_pass1w",
+                     "kernel": ("k_pass1s" if want else "k_pass1n") if B >= 512 * 64
+                               else ("k_pass1w" if want else "k_pass1n (wide)"),
                      "avg_launch_ms": round(pass1_ms, 4),
                      "algorithmic_bytes_per_launch": B * M},
         "pass1_share_of_step": round(pass1_ms / ms_per_step, 4),

@@ -28,7 +28,9 @@
  * loop, since novelty depends only on the order, which the batch keeps.
  *
  * Options (create's JSON string; every key optional):
- *   {"map_size": 65536, "max_batch": 4096, "ignore_bytes_file": "<path>" (dynamorio_gpu)}
+ *   {"map_size": 65536, "max_batch": 4096}; dynamorio_gpu also "ignore_bytes_file": "<path>",
+ *   "per_module_coverage": 0/1, "coverage_modules": [names], "ignore_bytes_dir": "<dir>",
+ *   "dump_map_dir": "<dir>" (dynamorio_instrumentation.c:1040-1051)
  * State (get_state / set_state / create's state argument), keys as the reference's
  * afl_get_state :62-79 and dynamorio_get_state :1239-1281:
  *   afl_gpu       {"map_size": M, "virgin_bits": "<hex>", "virgin_tmout": "<hex>",
@@ -83,7 +85,8 @@ typedef struct kbz_instrumentation {
                 size_t input_length);
   int (*is_new_path)(void *instrumentation_state);
   int (*get_fuzz_result)(void *instrumentation_state);
-  /* optional (instrumentation.h:58-61); NULL here, as in the afl plugin */
+  /* optional (instrumentation.h:58-61): NULL in afl_gpu (as in the afl plugin); dynamorio_gpu
+   * binds both, as instrumentation_factory.c:53-54 does for the dynamorio plugin */
   int (*get_module_info)(void *instrumentation_state, int index, int *is_new, char **module_name,
                          char **info, int *size);
   kbz_instrumentation_edges_t *(*get_edges)(void *instrumentation_state, int index);
@@ -153,6 +156,17 @@ int kbz_dynamorio_gpu_help(char **help_str);
 long kbz_dynamorio_gpu_record(void *state, const uint8_t *trace_bits, int fuzz_result);
 int kbz_dynamorio_gpu_result(void *state, long ticket);
 int kbz_dynamorio_gpu_flush(void *state);
+/* dynamorio_get_module_info (dynamorio_instrumentation.c:1541-1573): module `index`'s
+ * last_path_was_new for the last exec (is_new), its name, its trace map as has_new_coverage
+ * left it (classified, map_size bytes, valid until the next exec) and map_size; asking for is_new
+ * or info triages the queued execs first.  0 = found, 1 = no such module, -1 = error / no exec
+ * yet.  Without per_module_coverage: the coverage_modules names, is_new 0, info NULL (as the
+ * reference). */
+int kbz_dynamorio_gpu_get_module_info(void *state, int index, int *is_new, char **module_name,
+                                      char **info, int *size);
+/* dynamorio_get_edges (:1582-1606): NULL (edge lists are not offered; the reference returns NULL
+ * unless its "edges" option asked for them ahead of time). */
+kbz_instrumentation_edges_t *kbz_dynamorio_gpu_get_edges(void *state, int index);
 
 #ifdef __cplusplus
 }

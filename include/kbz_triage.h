@@ -24,6 +24,9 @@
  *       has_new_coverage_per_module (dynamorio_instrumentation.c:1477-1493): per-module maps
  *   kbz_picker_ignore_device
  *       the picker CLI's ignore-bytes diff across repeated runs (picker/main.c:240-262)
+ *   kbz_transform_rows_device / _host
+ *       classify_counts (dynamorio_instrumentation.c:265-292) / simplify_trace
+ *       (afl_instrumentation.c:674-706) over a batch of maps (get_module_info's info, dump_map_dir)
  *   kbz_hash32_device / kbz_xxh64_device
  *       afl_progs/hash.h:36-65 (hash32) and instrumentation/xxhash.c:855 (XXH64, v0.6.5)
  *       over every trace of a batch (crash/hang dedup keys).
@@ -43,7 +46,7 @@
 extern "C" {
 #endif
 
-#define KBZ_ABI_VERSION 2
+#define KBZ_ABI_VERSION 3
 
 /* Triage semantics (which reference code path a batch reproduces). */
 enum kbz_mode {
@@ -118,6 +121,11 @@ int kbz_ctx_time_pass1(kbz_ctx_t *ctx, int enable, double *total_ms, uint32_t *l
  *           (the value DynamoRIO compares with last_shm_hash).
  * x64_out:  device uint64[n] or NULL (needs KBZ_WANT_X64): XXH64(seed 0) of the transformed
  *           trace -- the crash/hang dedup key.
+ * want:     KBZ_WANT_* bits.  DYNAMORIO mode always computes hash32 (its last-hash skip needs
+ *           it).  The AFL modes hash only when asked (want & KBZ_WANT_H32, an XXH64 request, or
+ *           a non-NULL h32_out), like the reference AFL plugin, which never hashes
+ *           (afl_instrumentation.c:231-274): a batch with none of them runs a pass without the
+ *           serial hash chains.
  * Stream-ordered; the virgin maps and last hash advance as if the n execs ran in order. */
 int kbz_triage_batch_device(kbz_ctx_t *ctx, const uint8_t *traces, size_t n, size_t stride,
                             const int8_t *outcome, uint8_t *hnb_out, uint32_t *h32_out,
@@ -217,15 +225,31 @@ int kbz_merge_and_fill(uint8_t *out, size_t n, size_t state_bytes, kbz_merge_fil
  * hnb_out: device uint8[k*n], hnb_out[m*n + j] = module m's has_new_coverage result for exec j
  * (0/1/2; nonzero = last_path_was_new); any_out: device uint8[n] or NULL, the OR over modules
  * (the per-exec return value).  Stream-ordered. */
+/* h32_out: device uint32[k*n] or NULL, h32_out[m*n + j] = module m's hash32 of exec j (what
+ * has_new_coverage compares with last_shm_hash, :1441-1451; the dump_map_dir file name). */
 int kbz_triage_modules_device(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *traces, size_t n,
                               size_t stride, const size_t *module_offsets, const int8_t *outcome,
-                              uint8_t *hnb_out, uint8_t *any_out, void *stream);
+                              uint8_t *hnb_out, uint8_t *any_out, uint32_t *h32_out,
+                              void *stream);
 
-/* Host-memory variant (traces, module_offsets, outcome, hnb_out [k*n], any_out [n] all host
- * memory).  Synchronous. */
+/* Host-memory variant (traces, module_offsets, outcome, hnb_out [k*n], any_out [n], h32_out
+ * [k*n] all host memory).  Synchronous. */
 int kbz_triage_modules_host(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *traces, size_t n,
                             size_t stride, const size_t *module_offsets, const int8_t *outcome,
-                            uint8_t *hnb_out, uint8_t *any_out);
+                            uint8_t *hnb_out, uint8_t *any_out, uint32_t *h32_out);
+
+/* ---- transformed maps ------------------------------------------------------------------------ */
+/* out row j = transform of row j (len bytes; out may equal rows with the same stride):
+ * KBZ_XF_CLASSIFY = classify_counts (dynamorio_instrumentation.c:265-292, the map has_new_coverage
+ * leaves in trace_bits: get_module_info's info, :1565, and the dump_map_dir files, :1453-1458),
+ * KBZ_XF_SIMPLIFY = simplify_trace (afl_instrumentation.c:674-706), KBZ_XF_RAW = a copy.
+ * len, strides and pointers 16-byte multiples / aligned.  Device, stream-ordered. */
+enum kbz_xf { KBZ_XF_RAW = 0, KBZ_XF_CLASSIFY = 1, KBZ_XF_SIMPLIFY = 2 };
+int kbz_transform_rows_device(const uint8_t *rows, size_t n, size_t stride, size_t len, int xf,
+                              uint8_t *out, size_t out_stride, void *stream);
+/* Host memory in and out (staged through the device).  Synchronous. */
+int kbz_transform_rows_host(const uint8_t *rows, size_t n, size_t stride, size_t len, int xf,
+                            uint8_t *out, size_t out_stride);
 
 /* ---- picker: ignore bytes from repeated runs ------------------------------------------------ */
 /* The picker's diff loop (picker/main.c:240-262) for one module: runs = device

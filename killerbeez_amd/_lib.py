@@ -12,7 +12,7 @@ import re
 from . import build as _build
 
 _LIB = None
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # (name, restype, argtypes) for every function declared in include/kbz_triage.h
 _vp, _sz, _i, _u32, _u64 = C.c_void_p, C.c_size_t, C.c_int, C.c_uint32, C.c_uint64
@@ -47,8 +47,10 @@ SIGNATURES = [
     ("kbz_merge_and_device", _i, [_vp, _vp, _sz, _sz, _vp]),
     ("kbz_merge_and_host", _i, [_vp, _vp, _sz, _sz]),
     ("kbz_merge_and_fill", _i, [_vp, _sz, _sz, _vp, _vp]),
-    ("kbz_triage_modules_device", _i, [_vp, _sz, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp]),
-    ("kbz_triage_modules_host", _i, [_vp, _sz, _vp, _sz, _sz, _vp, _vp, _vp, _vp]),
+    ("kbz_triage_modules_device", _i, [_vp, _sz, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("kbz_triage_modules_host", _i, [_vp, _sz, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp]),
+    ("kbz_transform_rows_device", _i, [_vp, _sz, _sz, _sz, _i, _vp, _sz, _vp]),
+    ("kbz_transform_rows_host", _i, [_vp, _sz, _sz, _sz, _i, _vp, _sz]),
     ("kbz_picker_ignore_device", _i, [_vp, _sz, _sz, _sz, _vp, _vp, _vp, _vp]),
     ("kbz_hash32_device", _i, [_vp, _sz, _sz, _sz, _u32, _vp, _vp]),
     ("kbz_xxh64_device", _i, [_vp, _sz, _sz, _sz, _u64, _vp, _vp]),

@@ -83,96 +83,236 @@ typedef struct kbz_plugin {
   uint8_t *mq;             /* queued execs, max_batch rows */
   int8_t *mq_outcome;
   uint8_t *r_mhnb;         /* [nmod][max_batch] per-module results of the last window */
+  /* get_module_info (dynamorio_instrumentation.c:1541-1573): the last triaged exec's raw maps
+   * (all modules, back to back) and, computed on the GPU when first asked, its classified maps
+   * (has_new_coverage leaves trace_bits classified, :1434) */
+  uint8_t *last_raw, *last_cls;
+  unsigned long gen, cls_gen;  /* windows triaged so far / window last_cls was computed for */
+  int have_exec;           /* an exec was triaged (the reference's enable_called) */
+  char **cov_names;        /* coverage_modules without per_module_coverage: names only */
+  size_t ncov;
+  /* dump_map_dir (dynamorio_instrumentation.c:1043, :1453-1458): every exec that is not a
+   * last-hash skip writes its classified map to <dir>/<%08x hash>; dprev[m] = module m's last
+   * hash before the next window */
+  char *dump_dir;
+  uint32_t *dprev;
+  uint32_t *r_h32;         /* [nmod or 1][max_batch] hashes of the last window (dump_map_dir) */
+  int restored_status;     /* last_process_status of a loaded state, until the next exec */
 } kbz_plugin_t;
 
 static size_t nmaps(const kbz_plugin_t *p) { return p->mode == KBZ_MODE_DYNAMORIO ? 1 : 3; }
 
-/* ---- minimal JSON: flat objects with number / string values (the formats of this file) ---- */
-static const char *json_value(const char *json, const char *key) {
-  char pat[96];
-  snprintf(pat, sizeof(pat), "\"%s\"", key);
-  for (const char *p = json; (p = strstr(p, pat)); p++) {
-    const char *q = p + strlen(pat);
-    while (*q == ' ' || *q == '\t' || *q == '\n' || *q == '\r') q++;
-    if (*q != ':') continue;
-    q++;
-    while (*q == ' ' || *q == '\t' || *q == '\n' || *q == '\r') q++;
-    return q;
+/* ---- JSON: the state / option formats of this file ------------------------------------------
+ * A small validating reader: a key is looked up among the TOP-LEVEL members of an object only
+ * (state objects nest module objects whose keys repeat the top-level names), values are skipped
+ * with full syntax checks (strings with escapes, numbers, literals, nested objects / arrays up to
+ * a depth limit), and strings are decoded (\" \\ \/ \b \f \n \r \t \uXXXX, surrogate pairs to
+ * UTF-8).  Malformed text is "not found" / an error, never a read past the terminating NUL. */
+enum { kJsonMaxDepth = 64 };
+static const char *js_ws(const char *p) {
+  while (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r') p++;
+  return p;
+}
+static int js_hex4(const char *p, unsigned *out) {
+  unsigned v = 0;
+  for (int i = 0; i < 4; i++) {
+    const char c = p[i];
+    const int d = (c >= '0' && c <= '9') ? c - '0' : (c >= 'a' && c <= 'f') ? c - 'a' + 10
+                  : (c >= 'A' && c <= 'F') ? c - 'A' + 10 : -1;
+    if (d < 0) return -1;
+    v = v << 4 | (unsigned)d;
   }
-  return NULL;
+  *out = v;
+  return 0;
+}
+/* past the closing quote of the string at p (*p == '"'), or NULL */
+static const char *js_skip_string(const char *p) {
+  for (p++; *p != '"'; p++) {
+    if (!*p || (unsigned char)*p < 0x20) return NULL;
+    if (*p == '\\') {
+      p++;
+      if (*p == 'u') {
+        unsigned u;
+        if (js_hex4(p + 1, &u)) return NULL;
+        p += 4;
+      } else if (!strchr("\"\\/bfnrt", *p) || !*p) {
+        return NULL;
+      }
+    }
+  }
+  return p + 1;
+}
+/* past the JSON value at p, or NULL if it is malformed */
+static const char *js_skip(const char *p, int depth) {
+  p = js_ws(p);
+  if (depth > kJsonMaxDepth) return NULL;
+  if (*p == '"') return js_skip_string(p);
+  if (*p == '{' || *p == '[') {
+    const char close = *p == '{' ? '}' : ']';
+    p = js_ws(p + 1);
+    if (*p == close) return p + 1;
+    for (;;) {
+      if (close == '}') {
+        if (*p != '"' || !(p = js_skip_string(p))) return NULL;
+        p = js_ws(p);
+        if (*p != ':') return NULL;
+        p++;
+      }
+      if (!(p = js_skip(p, depth + 1))) return NULL;
+      p = js_ws(p);
+      if (*p == ',') {
+        p = js_ws(p + 1);
+        continue;
+      }
+      return *p == close ? p + 1 : NULL;
+    }
+  }
+  if (!strncmp(p, "true", 4)) return p + 4;
+  if (!strncmp(p, "false", 5)) return p + 5;
+  if (!strncmp(p, "null", 4)) return p + 4;
+  const char *q = p;
+  if (*q == '-') q++;
+  if (*q < '0' || *q > '9') return NULL;
+  while (*q >= '0' && *q <= '9') q++;
+  if (*q == '.') {
+    q++;
+    if (*q < '0' || *q > '9') return NULL;
+    while (*q >= '0' && *q <= '9') q++;
+  }
+  if (*q == 'e' || *q == 'E') {
+    q++;
+    if (*q == '+' || *q == '-') q++;
+    if (*q < '0' || *q > '9') return NULL;
+    while (*q >= '0' && *q <= '9') q++;
+  }
+  return q;
+}
+/* the value of top-level member `key` of the object `json`, or NULL (absent or malformed).  Keys
+ * are compared as written (the formats here never escape key characters). */
+static const char *json_value(const char *json, const char *key) {
+  if (!json) return NULL;
+  const size_t kl = strlen(key);
+  const char *p = js_ws(json);
+  if (*p != '{') return NULL;
+  p = js_ws(p + 1);
+  if (*p == '}') return NULL;
+  for (;;) {
+    if (*p != '"') return NULL;
+    const char *ks = p + 1, *ke = js_skip_string(p);
+    if (!ke) return NULL;
+    p = js_ws(ke);
+    if (*p != ':') return NULL;
+    const char *v = js_ws(p + 1);
+    if ((size_t)(ke - 1 - ks) == kl && !memcmp(ks, key, kl)) return v;
+    if (!(p = js_skip(v, 1))) return NULL;
+    p = js_ws(p);
+    if (*p != ',') return NULL;
+    p = js_ws(p + 1);
+  }
 }
 
-/* 1 found, 0 absent, -1 malformed */
+/* 1 found, 0 absent, -1 malformed (not a non-negative integer that fits) */
 static int json_u64(const char *json, const char *key, unsigned long long *out) {
   const char *v = json ? json_value(json, key) : NULL;
   if (!v) return 0;
-  char *end;
-  unsigned long long x = strtoull(v, &end, 10);
-  if (end == v) return -1;
+  if (*v < '0' || *v > '9') return -1;
+  unsigned long long x = 0;
+  for (; *v >= '0' && *v <= '9'; v++) {
+    if (x > (~0ull - (unsigned)(*v - '0')) / 10) return -1;
+    x = x * 10 + (unsigned)(*v - '0');
+  }
+  const char *e = js_ws(v);
+  if (*e != ',' && *e != '}') return -1;
   *out = x;
   return 1;
 }
 
-static char *json_str(const char *json, const char *key) {
-  const char *v = json ? json_value(json, key) : NULL;
-  if (!v || *v != '"') return NULL;
-  v++;
-  char *s = (char *)malloc(strlen(v) + 1);
-  if (!s) return NULL;
+/* the JSON string at s (*s == '"') -> malloc'd decoded UTF-8 text, NULL if malformed */
+static char *json_unquote(const char *s) {
+  if (!s || *s != '"') return NULL;
+  const char *end = js_skip_string(s);
+  if (!end) return NULL;
+  char *o = (char *)malloc((size_t)(end - s) * 2 + 1);  /* \uXXXX -> at most 3 bytes */
+  if (!o) return NULL;
   size_t n = 0;
-  for (; *v && *v != '"'; v++) {
-    if (*v == '\\' && v[1]) v++;
-    s[n++] = *v;
+  for (s++; s < end - 1; s++) {
+    if (*s != '\\') {
+      o[n++] = *s;
+      continue;
+    }
+    s++;
+    switch (*s) {
+      case 'b': o[n++] = '\b'; break;
+      case 'f': o[n++] = '\f'; break;
+      case 'n': o[n++] = '\n'; break;
+      case 'r': o[n++] = '\r'; break;
+      case 't': o[n++] = '\t'; break;
+      case 'u': {
+        unsigned u, lo;
+        js_hex4(s + 1, &u);
+        s += 4;
+        if (u >= 0xd800 && u < 0xdc00 && s[1] == '\\' && s[2] == 'u' && !js_hex4(s + 3, &lo) &&
+            lo >= 0xdc00 && lo < 0xe000) {
+          u = 0x10000 + ((u - 0xd800) << 10) + (lo - 0xdc00);
+          s += 6;
+        }
+        if (!u || (u >= 0xd800 && u < 0xe000)) {  /* NUL or a lone surrogate: reject */
+          free(o);
+          return NULL;
+        }
+        if (u < 0x80) {
+          o[n++] = (char)u;
+        } else if (u < 0x800) {
+          o[n++] = (char)(0xc0 | u >> 6);
+          o[n++] = (char)(0x80 | (u & 0x3f));
+        } else if (u < 0x10000) {
+          o[n++] = (char)(0xe0 | u >> 12);
+          o[n++] = (char)(0x80 | ((u >> 6) & 0x3f));
+          o[n++] = (char)(0x80 | (u & 0x3f));
+        } else {
+          o[n++] = (char)(0xf0 | u >> 18);
+          o[n++] = (char)(0x80 | ((u >> 12) & 0x3f));
+          o[n++] = (char)(0x80 | ((u >> 6) & 0x3f));
+          o[n++] = (char)(0x80 | (u & 0x3f));
+        }
+        break;
+      }
+      default: o[n++] = *s;  /* \" \\ \/ */
+    }
   }
-  s[n] = 0;
-  return s;
+  o[n] = 0;
+  return o;
 }
 
-/* The raw text of a JSON array value ("[...]") -> its top-level elements as malloc'd strings
- * (quotes kept for strings, braces for objects); NULL + *n = 0 when the key is absent. */
+static char *json_str(const char *json, const char *key) {
+  return json_unquote(json ? json_value(json, key) : NULL);
+}
+
+/* The elements of top-level array member `key` as malloc'd strings of their raw JSON text
+ * (quotes kept for strings, braces for objects); NULL + *n = 0 when the key is absent; *bad = 1
+ * when it is not a well-formed array. */
 static char **json_array(const char *json, const char *key, size_t *n, int *bad) {
   *n = 0;
   *bad = 0;
   const char *v = json ? json_value(json, key) : NULL;
   if (!v) return NULL;
-  if (*v != '[') {
+  if (*v != '[' || !js_skip(v, 1)) {
     *bad = 1;
     return NULL;
   }
   char **items = NULL;
-  const char *q = v + 1;
+  const char *q = js_ws(v + 1);
+  if (*q == ']') return (char **)calloc(1, sizeof(char *));  /* empty: non-NULL, n = 0 */
   for (;;) {
-    while (*q == ' ' || *q == '\t' || *q == '\n' || *q == '\r' || *q == ',') q++;
-    if (*q == ']') return items;
-    if (!*q) break;
-    const char *b = q;
-    int depth = 0, in_str = 0;
-    for (; *q; q++) {
-      if (in_str) {
-        if (*q == '\\' && q[1]) q++;
-        else if (*q == '"') in_str = 0;
-        if (!in_str && !depth) {
-          q++;
-          break;
-        }
-        continue;
-      }
-      if (*q == '"') in_str = 1;
-      else if (*q == '{' || *q == '[') depth++;
-      else if (*q == '}' || *q == ']') {
-        if (!depth) break;
-        if (!--depth) {
-          q++;
-          break;
-        }
-      } else if (*q == ',' && !depth) break;
-    }
+    const char *e = js_skip(q, 2);  /* well-formed: checked above */
     char **grown = (char **)realloc(items, (*n + 1) * sizeof(char *));
     if (!grown) break;
     items = grown;
-    items[*n] = strndup(b, (size_t)(q - b));
-    if (!items[*n]) break;
+    if (!(items[*n] = strndup(q, (size_t)(e - q)))) break;
     (*n)++;
+    q = js_ws(e);
+    if (*q == ']') return items;
+    q = js_ws(q + 1);  /* ',' */
   }
   *bad = 1;
   for (size_t i = 0; i < *n; i++) free(items[i]);
@@ -184,19 +324,6 @@ static void free_strings(char **v, size_t n) {
   if (!v) return;
   for (size_t i = 0; i < n; i++) free(v[i]);
   free(v);
-}
-/* a JSON string element ("...") -> malloc'd unescaped text */
-static char *json_unquote(const char *s) {
-  if (!s || *s != '"') return NULL;
-  char *o = (char *)malloc(strlen(s));
-  if (!o) return NULL;
-  size_t n = 0;
-  for (s++; *s && *s != '"'; s++) {
-    if (*s == '\\' && s[1]) s++;
-    o[n++] = *s;
-  }
-  o[n] = 0;
-  return o;
 }
 
 static int hexval(char c) {
@@ -245,6 +372,12 @@ static void plugin_free(kbz_plugin_t *p) {
   free(p->mq);
   free(p->mq_outcome);
   free(p->r_mhnb);
+  free(p->last_raw);
+  free(p->last_cls);
+  free_strings(p->cov_names, p->ncov);
+  free(p->dump_dir);
+  free(p->dprev);
+  free(p->r_h32);
   free(p->ignore);
   free(p->virgin);
   free(p->r_hnb);
@@ -287,6 +420,7 @@ static kbz_plugin_t *plugin_alloc(int mode, size_t map_size, size_t max_batch) {
   p->max_batch = max_batch;
   p->last_ticket = -1;
   p->last_fuzz_result = KBZ_PLUGIN_FUZZ_ERROR;
+  p->restored_status = 0;
   p->virgin = (uint8_t *)malloc(3 * map_size);
   p->r_hnb = (uint8_t *)malloc(max_batch);
   if (!p->virgin || !p->r_hnb) {
@@ -320,6 +454,20 @@ static int load_ignore(kbz_plugin_t *p, const char *path) {
   return p->ignore ? 0 : -1;
 }
 
+/* dump_map_dir: per-map last hashes and the window's hash buffer (frees p on failure) */
+static kbz_plugin_t *plugin_dump_alloc(kbz_plugin_t *p) {
+  if (!p->dump_dir) return p;
+  const size_t k = p->per_module ? p->nmod : 1;
+  p->dprev = (uint32_t *)calloc(k, sizeof(uint32_t));
+  p->r_h32 = (uint32_t *)malloc(k * p->max_batch * sizeof(uint32_t));
+  if (!p->dprev || !p->r_h32) {
+    set_err("out of host memory");
+    plugin_free(p);
+    return NULL;
+  }
+  return p;
+}
+
 static kbz_plugin_t *plugin_from_options(int mode, const char *options) {
   unsigned long long m = 65536, mb = 4096;
   if (json_u64(options, "map_size", &m) < 0 || json_u64(options, "max_batch", &mb) < 0) {
@@ -342,17 +490,12 @@ static kbz_plugin_t *plugin_from_options(int mode, const char *options) {
     plugin_free(p);
     return NULL;
   }
-  if (pm) {  /* dynamorio_instrumentation.c:1048-1063 */
-    size_t n = 0;
+  char **names = NULL;
+  size_t n = 0;
+  if (mode == KBZ_MODE_DYNAMORIO) {  /* coverage_modules, dump_map_dir (:1043, :1050) */
     int bad = 0;
     char **raw = json_array(options, "coverage_modules", &n, &bad);
-    if (bad || !n) {
-      free_strings(raw, n);
-      set_err("No Coverage Module selected, please specify one with the coverage_modules option.");
-      plugin_free(p);
-      return NULL;
-    }
-    char **names = (char **)calloc(n, sizeof(char *));
+    names = bad ? NULL : (char **)calloc(n ? n : 1, sizeof(char *));
     for (size_t i = 0; names && i < n; i++) names[i] = json_unquote(raw[i]);
     free_strings(raw, n);
     int ok = names != NULL;
@@ -363,6 +506,24 @@ static kbz_plugin_t *plugin_from_options(int mode, const char *options) {
       plugin_free(p);
       return NULL;
     }
+    if (json_value(options, "dump_map_dir") && !(p->dump_dir = json_str(options, "dump_map_dir"))) {
+      free_strings(names, n);
+      set_err("dump_map_dir must be a string");
+      plugin_free(p);
+      return NULL;
+    }
+  }
+  if (pm && !n) {
+    free_strings(names, n);
+    set_err("No Coverage Module selected, please specify one with the coverage_modules option.");
+    plugin_free(p);
+    return NULL;
+  }
+  if (!pm) {  /* names only: get_module_info reports them (no per-module maps) */
+    p->cov_names = names;
+    p->ncov = n;
+  }
+  if (pm) {  /* dynamorio_instrumentation.c:1048-1063 */
     if (plugin_modules(p, names, n)) {
       plugin_free(p);
       return NULL;
@@ -381,7 +542,7 @@ static kbz_plugin_t *plugin_from_options(int mode, const char *options) {
       }
     }
     free(dir);
-    return p;
+    return plugin_dump_alloc(p);
   }
   char *ign = mode == KBZ_MODE_DYNAMORIO ? json_str(options, "ignore_bytes_file") : NULL;
   if (ign) {
@@ -392,12 +553,28 @@ static kbz_plugin_t *plugin_from_options(int mode, const char *options) {
       return NULL;
     }
   }
-  return p;
+  return plugin_dump_alloc(p);
 }
 
 /* a fresh state with the same configuration (merge results) */
 static kbz_plugin_t *plugin_clone_config(const kbz_plugin_t *src) {
   kbz_plugin_t *p = plugin_alloc(src->mode, src->map_size, src->max_batch);
+  if (p && src->ncov) {
+    p->cov_names = (char **)calloc(src->ncov, sizeof(char *));
+    for (size_t i = 0; p->cov_names && i < src->ncov; i++) {
+      if (!(p->cov_names[i] = strdup(src->cov_names[i]))) {
+        free_strings(p->cov_names, i);
+        p->cov_names = NULL;
+        break;
+      }
+    }
+    if (!p->cov_names) {
+      plugin_free(p);
+      set_err("out of host memory");
+      return NULL;
+    }
+    p->ncov = src->ncov;
+  }
   if (p && src->per_module) {
     char **names = (char **)calloc(src->nmod, sizeof(char *));
     for (size_t i = 0; names && i < src->nmod; i++) names[i] = strdup(src->mod_names[i]);
@@ -505,27 +682,81 @@ static int sync_mirror(kbz_plugin_t *p) {
   return 0;
 }
 
+/* After a triaged window of n execs (rows of the k module maps back to back, `stride` apart):
+ * remember the last exec's raw maps for get_module_info (dynamorio_instrumentation.c:1541-1573)
+ * and, with dump_map_dir, write the classified map (has_new_coverage classifies trace_bits in
+ * place, :1434) of every exec whose hash differs from the previous exec's -- the execs
+ * has_new_coverage does not skip (:1450-1451) -- to <dir>/<%08x hash> (:1453-1458), in exec
+ * order (a later exec with the same hash overwrites the file, as the reference's writes do).
+ * The maps are classified on the GPU; p->r_h32 holds the window's hashes ([k][n]). */
+static int plugin_window_done(kbz_plugin_t *p, const uint8_t *rows, size_t n, size_t stride) {
+  const size_t k = p->per_module ? p->nmod : 1, m = p->map_size, row = k * m;
+  if (!n) return 0;
+  p->have_exec = 1;
+  p->gen++;
+  if (p->per_module) {
+    if (!p->last_raw && !(p->last_raw = (uint8_t *)malloc(row))) {
+      set_err("out of host memory");
+      return -1;
+    }
+    memcpy(p->last_raw, rows + (n - 1) * stride, row);
+  }
+  if (!p->dump_dir) return 0;
+  uint8_t *cls = (uint8_t *)malloc(n * row);
+  if (!cls) {
+    set_err("out of host memory");
+    return -1;
+  }
+  if (kbz_transform_rows_host(rows, n, stride, row, KBZ_XF_CLASSIFY, cls, row)) {
+    set_err("GPU classify (dump_map_dir): %s", kbz_last_error());
+    free(cls);
+    return -1;
+  }
+  for (size_t q = 0; q < k; q++) {
+    uint32_t prev = p->dprev[q];
+    for (size_t j = 0; j < n; j++) {
+      const uint32_t h = p->r_h32[q * n + j];
+      if (h == prev) continue;  /* a last-hash skip: nothing is written */
+      prev = h;
+      char path[4096];
+      snprintf(path, sizeof(path), "%s/%08x", p->dump_dir, h);
+      FILE *f = fopen(path, "wb");  /* the reference ignores a failed write too */
+      if (f) {
+        (void)fwrite(cls + j * row + q * m, 1, m, f);
+        fclose(f);
+      }
+    }
+    p->dprev[q] = prev;
+  }
+  free(cls);
+  return 0;
+}
+
 /* Triage the queued execs (the acquired ring slot) as one ordered batch and wait for it.  A
  * batch of at most 64 execs is read by the GPU straight from the pinned slot (no DMA). */
 static int plugin_flush(kbz_plugin_t *p) {
   if (!p->q_rows) return 0;
   p->mirror_stale = 1;
   const size_t n = p->q_n;
+  const uint8_t *rows = p->q_rows;  /* the slot stays valid until the next record */
   p->q_rows = NULL;
   p->q_n = 0;
   if (p->per_module) {  /* has_new_coverage_per_module over the batch */
     size_t offs[p->nmod];
     for (size_t i = 0; i < p->nmod; i++) offs[i] = i * p->map_size;
     if (kbz_triage_modules_host(p->mctx, p->nmod, p->mq, n, p->nmod * p->map_size, offs,
-                                p->mq_outcome, p->r_mhnb, p->r_hnb)) {
+                                p->mq_outcome, p->r_mhnb, p->r_hnb, p->dump_dir ? p->r_h32 : NULL)) {
       set_err("GPU triage: %s", kbz_last_error());
       return -1;
     }
     for (size_t i = 0; i < p->nmod; i++) p->mnew[i] = p->r_mhnb[i * n + n - 1] != 0;
-  } else if (kbz_ring_submit(p->ctx, n, 1, p->r_hnb, NULL, NULL, 0) || kbz_ring_flush(p->ctx)) {
+  } else if (kbz_ring_submit(p->ctx, n, 1, p->r_hnb, p->dump_dir ? p->r_h32 : NULL, NULL,
+                             p->dump_dir ? KBZ_WANT_H32 : 0) ||
+             kbz_ring_flush(p->ctx)) {
     set_err("GPU triage: %s", kbz_last_error());
     return -1;
   }
+  if (plugin_window_done(p, rows, n, (p->per_module ? p->nmod : 1) * p->map_size)) return -1;
   p->last_path_was_new = p->r_hnb[n - 1] != 0;
   p->r_base = p->q_base;
   p->r_n = n;
@@ -603,25 +834,89 @@ static int plugin_triage_batch(kbz_plugin_t *p, const uint8_t *traces, size_t n,
       const size_t cnt = n - lo < p->max_batch ? n - lo : p->max_batch;
       if (kbz_triage_modules_host(p->mctx, p->nmod, traces + lo * stride, cnt, stride, offs,
                                   outcome ? outcome + lo : NULL, p->r_mhnb,
-                                  hnb ? hnb + lo : p->r_hnb)) {
+                                  hnb ? hnb + lo : p->r_hnb, p->dump_dir ? p->r_h32 : NULL)) {
         set_err("GPU triage: %s", kbz_last_error());
         return -1;
       }
       for (size_t i = 0; i < p->nmod; i++) p->mnew[i] = p->r_mhnb[i * cnt + cnt - 1] != 0;
+      if (plugin_window_done(p, traces + lo * stride, cnt, stride)) return -1;
     }
     return 0;
   }
-  const int want = (h32 ? KBZ_WANT_H32 : 0) | (x64 ? KBZ_WANT_X64 : 0);
+  const int want = (h32 || p->dump_dir ? KBZ_WANT_H32 : 0) | (x64 ? KBZ_WANT_X64 : 0);
   for (size_t lo = 0; lo < n; lo += p->max_batch) {
     const size_t cnt = n - lo < p->max_batch ? n - lo : p->max_batch;
+    uint32_t *hb = h32 ? h32 + lo : p->dump_dir ? p->r_h32 : NULL;
     if (kbz_triage_batch_host(p->ctx, traces + lo * stride, cnt, stride,
-                              outcome ? outcome + lo : NULL, hnb ? hnb + lo : NULL,
-                              h32 ? h32 + lo : NULL, x64 ? x64 + lo : NULL, want)) {
+                              outcome ? outcome + lo : NULL, hnb ? hnb + lo : NULL, hb,
+                              x64 ? x64 + lo : NULL, want)) {
       set_err("GPU triage: %s", kbz_last_error());
       return -1;
     }
+    if (p->dump_dir && hb != p->r_h32) memcpy(p->r_h32, hb, cnt * sizeof(uint32_t));
+    if (plugin_window_done(p, traces + lo * stride, cnt, stride)) return -1;
   }
   return 0;
+}
+
+/* get_module_info (dynamorio_instrumentation.c:1541-1573): asking for is_new or info finishes the
+ * round first (finish_fuzz_round: here, triage the queued execs); -1 before any exec.  With
+ * per_module_coverage: the module's last_path_was_new for the last exec, its name, its trace map
+ * as has_new_coverage left it (classified, :1434; classified on the GPU when first asked, kept
+ * until the next triaged exec) and map_size; 1 for an index past the modules.  Without it the
+ * coverage_modules are reported with is_new 0 and no map, as the reference does (per-module
+ * trace maps and last_path_was_new exist only with per_module_coverage, :453-470, :1488). */
+static int plugin_module_info(kbz_plugin_t *p, int index, int *is_new, char **module_name,
+                              char **info, int *size) {
+  if (!p) {
+    set_err("null state");
+    return -1;
+  }
+  if (info || is_new) {
+    if (plugin_flush(p)) return -1;
+    if (!p->have_exec) {
+      set_err("no exec has been triaged yet");
+      return -1;
+    }
+  }
+  const size_t m = p->map_size;
+  if (p->per_module) {
+    if (index < 0 || (size_t)index >= p->nmod) return 1;
+    if (is_new) *is_new = p->mnew[index];
+    if (module_name) *module_name = p->mod_names[index];
+    if (info) {
+      const size_t row = p->nmod * m;
+      if (p->cls_gen != p->gen || !p->last_cls) {
+        if (!p->last_cls && !(p->last_cls = (uint8_t *)malloc(row))) {
+          set_err("out of host memory");
+          return -1;
+        }
+        if (kbz_transform_rows_host(p->last_raw, 1, row, row, KBZ_XF_CLASSIFY, p->last_cls, row)) {
+          set_err("GPU classify: %s", kbz_last_error());
+          return -1;
+        }
+        p->cls_gen = p->gen;
+      }
+      *info = (char *)p->last_cls + (size_t)index * m;
+    }
+    if (size) *size = (int)m;
+    return 0;
+  }
+  if (index < 0 || (size_t)index >= p->ncov) return 1;
+  if (is_new) *is_new = 0;
+  if (module_name) *module_name = p->cov_names[index];
+  if (info) *info = NULL;
+  if (size) *size = (int)m;
+  return 0;
+}
+
+/* get_edges (dynamorio_instrumentation.c:1582-1606): edge lists exist only when the "edges"
+ * option asked for them ahead of time, which this plugin does not offer: NULL, as the reference
+ * returns without it. */
+static kbz_instrumentation_edges_t *plugin_edges(kbz_plugin_t *p, int index) {
+  (void)p, (void)index;
+  set_err("no edge list: the edges option is not supported (trace maps only)");
+  return NULL;
 }
 
 /* ---- state --------------------------------------------------------------------------------- */
@@ -644,7 +939,8 @@ static char *plugin_get_state(kbz_plugin_t *p) {
   /* last_process_status: the FUZZ_* result of the last exec (dynamorio_get_state :1249) */
   char *o = s + sprintf(s, "{\"map_size\":%zu", m);
   if (p->mode == KBZ_MODE_DYNAMORIO)
-    o += sprintf(o, ",\"last_process_status\":%d", p->last_ticket >= 0 ? p->last_fuzz_result : 0);
+    o += sprintf(o, ",\"last_process_status\":%d",
+                 p->last_ticket >= 0 ? p->last_fuzz_result : p->restored_status);
   if (p->per_module) {  /* dynamorio_get_state :1260-1275 */
     o += sprintf(o, ",\"modules\":[");
     for (size_t i = 0; i < p->nmod; i++) {
@@ -748,11 +1044,16 @@ static int plugin_set_state(kbz_plugin_t *p, const char *json) {
   }
   /* execs recorded before the new state was loaded belong to the old one */
   if (plugin_flush(p)) return 1;
-  if (json_u64(json, "last_process_status", &ls) < 0) {
+  if (json_u64(json, "last_process_status", &ls) < 0 || ls > 0x7fffffff) {
     set_err("bad last_process_status");
     return 1;
   }
-  if (p->per_module) return set_state_modules(p, json);
+  if (p->per_module) {
+    if (set_state_modules(p, json)) return 1;
+    p->restored_status = (int)ls;  /* dynamorio_set_state :1325 */
+    if (p->dprev) memcpy(p->dprev, p->mlast, p->nmod * sizeof(uint32_t));
+    return 0;
+  }
   const size_t ms = p->map_size, k = nmaps(p);
   uint8_t *v = (uint8_t *)malloc(3 * ms);
   if (!v) {
@@ -783,6 +1084,8 @@ static int plugin_set_state(kbz_plugin_t *p, const char *json) {
   p->last_hash = (uint32_t)h;
   p->last_path_was_new = lw != 0;
   p->mirror_stale = 0;
+  p->restored_status = (int)ls;  /* dynamorio_set_state :1325 (reported until the next exec) */
+  if (p->dprev) p->dprev[0] = p->last_hash;
   return 0;
 }
 
@@ -1044,7 +1347,9 @@ static const char kHelpDr[] =
     "  per_module_coverage   1: one map per coverage module (record() takes the modules'\n"
     "                        maps back to back, in coverage_modules order)\n"
     "  coverage_modules      Array of module names (per_module_coverage)\n"
-    "  ignore_bytes_dir      Directory of <module>.dat ignore bytes files (per_module_coverage)\n";
+    "  ignore_bytes_dir      Directory of <module>.dat ignore bytes files (per_module_coverage)\n"
+    "  dump_map_dir          Directory: every exec that is not a last-hash skip writes its\n"
+    "                        classified map to <dir>/<hash32 as %08x>\n";
 
 static int plugin_help(int mode, char **help_str) {
   if (!help_str) return -1;
@@ -1101,6 +1406,15 @@ static int plugin_help(int mode, char **help_str) {
 KBZ_PLUGIN_ENTRY_POINTS(kbz_afl_gpu, KBZ_MODE_AFL, "afl_gpu")
 KBZ_PLUGIN_ENTRY_POINTS(kbz_dynamorio_gpu, KBZ_MODE_DYNAMORIO, "dynamorio_gpu")
 
+/* the DynamoRIO plugin's optional members (instrumentation_factory.c:53-54 binds them) */
+int kbz_dynamorio_gpu_get_module_info(void *s, int index, int *is_new, char **module_name,
+                                      char **info, int *size) {
+  return plugin_module_info((kbz_plugin_t *)s, index, is_new, module_name, info, size);
+}
+kbz_instrumentation_edges_t *kbz_dynamorio_gpu_get_edges(void *s, int index) {
+  return plugin_edges((kbz_plugin_t *)s, index);
+}
+
 #define KBZ_FILL_VTABLE(r, P)          \
   do {                                 \
     (r)->create = P##_create;          \
@@ -1128,6 +1442,8 @@ kbz_instrumentation_t *kbz_instrumentation_factory(const char *name) {
     KBZ_FILL_VTABLE(r, kbz_afl_gpu);
   } else if (!strcmp(name, "dynamorio_gpu")) {
     KBZ_FILL_VTABLE(r, kbz_dynamorio_gpu);
+    r->get_module_info = kbz_dynamorio_gpu_get_module_info;
+    r->get_edges = kbz_dynamorio_gpu_get_edges;
   } else {
     free(r);
     set_err("unknown instrumentation %s", name);

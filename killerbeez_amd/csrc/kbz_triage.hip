@@ -125,6 +125,19 @@ __device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[2]) {
   asm volatile("s_waitcnt vmcnt(%2)" : "+v"(r[0]), "+v"(r[1]) : "n"(N) : "memory");
 }
 template <int N>
+__device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[17]) {  // k_pass1n: 16 rows + virgin
+  asm volatile("s_waitcnt vmcnt(%17)"
+               : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
+                 "+v"(r[6]), "+v"(r[7]), "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]),
+                 "+v"(r[12]), "+v"(r[13]), "+v"(r[14]), "+v"(r[15]), "+v"(r[16])
+               : "n"(N)
+               : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[3]) {
+  asm volatile("s_waitcnt vmcnt(%3)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]) : "n"(N) : "memory");
+}
+template <int N>
 __device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[4]) {
   asm volatile("s_waitcnt vmcnt(%4)"
                : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3])
@@ -1028,6 +1041,204 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// pass 1 without hashes: AFL / AFL_CLASSIFY batches for which neither hash32 nor XXH64 is wanted
+// (the reference AFL plugin never hashes: finish_fuzz_round, afl_instrumentation.c:231-274).
+// Nothing is serial, so the waves of a chunk need not share a tile: wave w owns a contiguous
+// range of the map's tiles (whole 64-tile flag words, so the waves write disjoint tile-flag
+// words) and streams all 64 rows of each of its tiles into a D-deep register ring -- ring
+// register i holds 16-B slot l % 16 of row 4 i + l / 16 in lane l, the same rows for the whole
+// kernel -- plus the tile's virgin words (lane l < 48: class l / 16, slot l % 16).  The column ORs
+// come from registers: per lane an OR over its 16 rows with per-lane class masks (class 0: the raw
+// row, AFL_CLASSIFY: classified), then across the 4 lanes sharing a slot (permlane16 / 32 swaps).
+// Simplified classes (HANG / CRASH rows, simplify_trace :668-706) need no per-row transform: OR
+// over rows of simplify(x) is, per byte, 0x80 where some row is nonzero and 0x01 where some row
+// is zero, so each lane keeps the OR of the class's raw rows and the AND of their "byte nonzero"
+// bits, only over ring registers that hold a row of that class (usually one or two).  Lane group
+// g = l / 16 then finishes class g of the tile: chunk_or where V still has bits, the tile flag,
+// the segment atomics.  No LDS, no barrier: every wave streams on its own.
+// NW = 2 for batches of many chunks (4 chunks per CU), 8 for the wide case (one chunk per CU).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t or_xor16_32(uint32_t v) {  // OR of lanes l, l^16, l^32, l^48
+  const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  const uint32_t w = a[0] | a[1];
+  const auto b = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+  return b[0] | b[1];
+}
+__device__ __forceinline__ uint32_t and_xor16_32(uint32_t v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  const uint32_t w = a[0] & a[1];
+  const auto b = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+  return b[0] & b[1];
+}
+// bit 7 of every byte: the byte is nonzero (other bits: don't care)
+__device__ __forceinline__ uint32_t nz_hi7(uint32_t x) {
+  return ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x;
+}
+__device__ __forceinline__ u32x4 or_lanes(u32x4 v) {
+  return u32x4{or_xor16_32(v.x), or_xor16_32(v.y), or_xor16_32(v.z), or_xor16_32(v.w)};
+}
+__device__ __forceinline__ u32x4 and_lanes(u32x4 v) {
+  return u32x4{and_xor16_32(v.x), and_xor16_32(v.y), and_xor16_32(v.z), and_xor16_32(v.w)};
+}
+// simplify's OR over rows from the raw rows' OR and the AND of their "nonzero" bits
+__device__ __forceinline__ u32x4 simp_or(u32x4 o, u32x4 z) {
+  const u32x4 nz = u32x4{nz_hi7(o.x), nz_hi7(o.y), nz_hi7(o.z), nz_hi7(o.w)} & 0x80808080u;
+  return nz | ((~z >> 7) & 0x01010101u);
+}
+
+#ifndef KBZ_N_ABL  // timing-only ablations of k_pass1n (wrong results): 1 = no simplified-class
+#define KBZ_N_ABL 0  // reduce, 2 = no class-0 reduce
+#endif
+template <int MODE, int NW, int D>
+__global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
+  static_assert(MODE != KBZ_MODE_DYNAMORIO, "DynamoRIO always hashes (last-hash skip)");
+  constexpr int NC = 3, TW = 256, SLOTS = 16, RPI = 4, NLD = kChunk / RPI, NR = NLD + 1;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t chunk = blockIdx.x;
+  const uint64_t row0 = (uint64_t)chunk * kChunk;
+  const int nrows = (int)min((uint64_t)kChunk, (uint64_t)a.n - row0);
+  const uint32_t ntiles = a.map_size / TW;
+  // this wave's tiles [t0, t1): whole flag words (64 tiles each; a.nfw words per class)
+  const uint32_t t0 = min(ntiles, a.nfw * wave / NW * 64);
+  const uint32_t t1 = min(ntiles, a.nfw * (wave + 1) / NW * 64);
+  const uint32_t nb = (t1 - t0 + D - 1) / D * D;  // steps, a multiple of D (0 for an idle wave)
+  // classes present in the chunk (wave-uniform; lane = row)
+  const int ocl = (lane < nrows && a.outcome) ? a.outcome[row0 + lane] : KBZ_FUZZ_NONE;
+  const int clane = class_of(MODE, ocl);
+  uint64_t present[NC];
+#pragma unroll
+  for (int k = 0; k < NC; k++) present[k] = __ballot(lane < nrows && clane == k);
+  if (wave == 0 && lane == 0) {
+    uint8_t m = 0;
+#pragma unroll
+    for (int k = 0; k < NC; k++) m |= present[k] ? (1u << k) : 0u;
+    a.chunk_cls[chunk] = m;
+    if (row0 + kChunk >= (uint64_t)a.n) a.shard_last[1] = 1;  // non-empty (no hash to report)
+  }
+  // this lane's rows (register i: row 4 i + lr; past the end of a partial chunk: the last row,
+  // masked out) and their classes: per lane bit i of cbits[k], per wave bit i of regs[k]
+  const int lr = lane / SLOTS, ls = lane % SLOTS;
+  const uint8_t *lbase = a.traces + row0 * a.stride + ls * 16;
+  uint32_t cbits[NC], regs[NC];
+#pragma unroll
+  for (int k = 0; k < NC; k++) cbits[k] = regs[k] = 0;
+#pragma unroll
+  for (int i = 0; i < NLD; i++) {
+    const int r = RPI * i + lr;
+    const int c = (r < nrows) ? class_of(MODE, a.outcome ? a.outcome[row0 + r] : KBZ_FUZZ_NONE)
+                              : -1;
+#pragma unroll
+    for (int k = 0; k < NC; k++) {
+      cbits[k] |= (c == k) ? (1u << i) : 0u;
+      regs[k] |= __ballot(c == k) ? (1u << i) : 0u;
+    }
+  }
+  // all-ones where bit i of cbits[k] is set: one v_bfe_i32 at the use (volatile: kept in the
+  // loop; hoisted, the masks and their complements cost more VGPRs than the ring)
+  auto msk = [&](int k, int i) -> uint32_t {
+    uint32_t m;
+    asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(cbits[k]), "n"(i));
+    return m;
+  };
+  const uint32_t vl = min(lane, 16 * NC - 1);
+  const uint8_t *vbase = a.vcur + (size_t)(vl / 16) * a.map_size + (vl % 16) * 16;
+  const uint32_t rstep = (uint32_t)(RPI * a.stride);  // <= 128 MiB
+  const uint32_t rlast = (uint32_t)((nrows - 1) * a.stride);
+  // branch-free asm loads (see k_pass1s); tiles past t1 re-load tile t0
+  auto load = [&](u32x4 (&r)[NR], uint32_t t) {
+    const uint32_t tt = t < t1 ? t : t0;
+#pragma unroll
+    for (int i = 0; i < NLD; i++) {
+      const uint32_t off = min((uint32_t)(i * rstep + lr * a.stride), rlast);
+      asm_load16(r[i], lbase + (size_t)tt * TW + off);
+    }
+    asm_load16_cached(r[NLD], vbase + (size_t)tt * TW);
+  };
+  const uint32_t seg = chunk / a.seg_len;
+  uint64_t *tfbase = a.tflags + (size_t)chunk * NC * a.nfw;
+  uint64_t tfl[NC];
+#pragma unroll
+  for (int k = 0; k < NC; k++) tfl[k] = 0;
+  const int g = lane / 16;  // the class this lane group finishes
+  u32x4 R[D][NR];
+#pragma unroll
+  for (int d = 0; d < D; d++) load(R[d], t0 + d);
+  for (uint32_t s0 = 0; s0 < nb; s0 += D) {
+#pragma unroll
+    for (int u = 0; u < D; u++) {
+      const uint32_t t = t0 + s0 + u;
+      vmcnt_wait_ring<(D - 1) * NR>(R[u]);
+      // ---- column ORs of tile t over the chunk's rows, per class
+      u32x4 o0 = {0, 0, 0, 0};
+#pragma unroll
+      for (int i = 0; i < ((KBZ_N_ABL & 2) ? 0 : NLD); i++) {
+        u32x4 x = R[u][i];
+        if (MODE == KBZ_MODE_AFL_CLASSIFY)
+          x = u32x4{classify4(x.x), classify4(x.y), classify4(x.z), classify4(x.w)};
+        o0 |= x & msk(0, i);
+      }
+      u32x4 fin[NC];
+      fin[0] = or_lanes(o0);
+#pragma unroll
+      for (int k = 1; k < NC; k++) {
+        fin[k] = u32x4{0, 0, 0, 0};
+        if (!present[k] || (KBZ_N_ABL & 1)) continue;  // wave-uniform, per chunk
+        u32x4 ok = {0, 0, 0, 0}, zk = {~0u, ~0u, ~0u, ~0u};
+#pragma unroll
+        for (int i = 0; i < NLD; i++) {
+          if (!(regs[k] & (1u << i))) continue;  // wave-uniform: no row of class k here
+          const u32x4 x = R[u][i];
+          const uint32_t mk = msk(k, i);
+          ok |= x & mk;
+          const u32x4 y = x | ~mk;
+          zk &= u32x4{nz_hi7(y.x), nz_hi7(y.y), nz_hi7(y.z), nz_hi7(y.w)};
+        }
+        fin[k] = simp_or(or_lanes(ok), and_lanes(zk));
+      }
+      // lane group g keeps class g's OR, masked with V (still-virgin bits only, like k_pass1s)
+      u32x4 m = g == 0 ? fin[0] : g == 1 ? fin[1] : fin[2];
+      m &= R[u][NLD];
+      if (g >= NC) m = u32x4{0, 0, 0, 0};
+      // m is complete here, so no value of the slot is still live when its registers are
+      // reloaded (otherwise the compiler renames the slot and copies it while loads fly)
+      asm volatile("" : "+v"(m));
+      load(R[u], t + D);  // the ring slot is free again
+      if (s0 + u < t1 - t0) {
+        const bool any = (m.x | m.y | m.z | m.w) != 0;
+        const uint64_t bal = __ballot(any);
+        const size_t off = (size_t)g * a.map_size + (size_t)t * TW + (size_t)ls * 16;
+        if (bal) {  // (rare) a class whose tile has still-virgin bits: its whole 256 B row
+          if ((bal >> (16 * g)) & 0xffffull)
+            *(uint4 *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) =
+                make_uint4(m.x, m.y, m.z, m.w);
+          if (any) {
+            unsigned long long *sp =
+                (unsigned long long *)(a.segor + (size_t)seg * NC * a.map_size + off);
+            const uint64_t lo = (uint64_t)m.x | ((uint64_t)m.y << 32);
+            const uint64_t hi = (uint64_t)m.z | ((uint64_t)m.w << 32);
+            if (lo) atomicOr(sp, (unsigned long long)lo);
+            if (hi) atomicOr(sp + 1, (unsigned long long)hi);
+          }
+#pragma unroll
+          for (int k = 0; k < NC; k++)
+            if ((bal >> (16 * k)) & 0xffffull) tfl[k] |= 1ull << (t & 63);
+        }
+        if ((t & 63) == 63 || t + 1 == t1) {
+          if (lane < NC) {
+            const uint64_t f = lane == 0 ? tfl[0] : lane == 1 ? tfl[1] : tfl[2];
+            if (present[lane]) tfbase[lane * a.nfw + (t >> 6)] = f;
+          }
+#pragma unroll
+          for (int k = 0; k < NC; k++) tfl[k] = 0;
+        }
+      }
+    }
+  }
+  drain_asm_loads(R);
+}
+
 // DynamoRIO last-hash skip: skip[j] = hash[j] == hash[j-1] (hash[-1] = previous exec's).
 // A skipped trace must not touch the virgin map.  Pass 1 OR'ed it into its chunk, which is
 // harmless when it equals its predecessor on the bytes has_new_bits examines (neq[j] == 0, exact
@@ -1650,6 +1861,24 @@ __global__ __launch_bounds__(256) void k_picker_final(uint32_t *words, size_t nw
   if (total && (threadIdx.x & 63) == 0 && c) atomicAdd(total, (unsigned long long)c);
 }
 
+// ---- transform rows: classify_counts / simplify_trace applied to a batch of maps -------------
+// 16 B per thread, grid (columns / 256 threads, rows).  The all-zero-word skip of classify_counts
+// (dynamorio_instrumentation.c:273) gives the same bytes (classify(0) = 0); simplify writes its
+// 0x01 bytes into all-zero words too (afl_instrumentation.c:688).
+__global__ __launch_bounds__(256) void k_transform_rows(const uint8_t *rows, size_t n, size_t stride,
+                                                        size_t len, int xf, uint8_t *out,
+                                                        size_t out_stride) {
+  const size_t col = (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (col >= len) return;
+  for (size_t r = blockIdx.y; r < n; r += gridDim.y) {
+    const uint4 v = *(const uint4 *)(rows + r * stride + col);
+    const uint64_t lo = xform8((uint64_t)v.x | ((uint64_t)v.y << 32), xf);
+    const uint64_t hi = xform8((uint64_t)v.z | ((uint64_t)v.w << 32), xf);
+    *(uint4 *)(out + r * out_stride + col) =
+        make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+  }
+}
+
 // ---- standalone row hashes (utility path: one lane per row, direct loads) ---------------------
 __global__ void k_rowhash32(const uint8_t *rows, size_t n, size_t stride, size_t len, uint32_t seed,
                             uint32_t *out) {
@@ -1917,8 +2146,34 @@ void launch_pass1(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s
 #endif
 }
 
-int pass1_dispatch(kbz_ctx *c, const Pass1Args &a, uint32_t chunks, bool x64, hipStream_t s) {
+#ifndef KBZ_PASS1N_D  // register ring depth of k_pass1n, narrow (2 waves per chunk) / wide (8)
+#define KBZ_PASS1N_D 2
+#endif
+#ifndef KBZ_PASS1N_WD
+#define KBZ_PASS1N_WD 2
+#endif
+template <int MODE>
+void launch_pass1n(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s) {
+  if (pass1_is_wide(choice, chunks))
+    hipLaunchKernelGGL((k_pass1n<MODE, 8, KBZ_PASS1N_WD>), dim3(chunks), dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_pass1n<MODE, 2, KBZ_PASS1N_D>), dim3(chunks), dim3(128), 0, s, a);
+}
+
+// hashed == false: an AFL-mode batch that wants neither hash (k_pass1n)
+int pass1_dispatch(kbz_ctx *c, const Pass1Args &a, uint32_t chunks, bool x64, bool hashed,
+                   hipStream_t s) {
   const bool ign = c->ignore != nullptr && c->mode == KBZ_MODE_DYNAMORIO;
+  if (!hashed && c->mode == KBZ_MODE_AFL) {
+    launch_pass1n<KBZ_MODE_AFL>(c->pass1, a, chunks, s);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+  if (!hashed && c->mode == KBZ_MODE_AFL_CLASSIFY) {
+    launch_pass1n<KBZ_MODE_AFL_CLASSIFY>(c->pass1, a, chunks, s);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
   switch (c->mode) {
     case KBZ_MODE_AFL:
       x64 ? launch_pass1<KBZ_MODE_AFL, false, true>(c->pass1, a, chunks, s)
@@ -2138,9 +2393,13 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
   a.map_size = (uint32_t)c->M;
   a.outcome = outcome;
   a.ignore = c->ignore;
-  a.h32 = h32_out ? h32_out : c->h32;  // hashes go straight to the caller's buffer
-  c->cur_h32 = a.h32;
   a.x64 = (want & KBZ_WANT_X64) ? x64_out : nullptr;
+  // AFL modes hash only on request (the reference AFL plugin never hashes); DynamoRIO always
+  // does (the last-hash skip)
+  const bool hashed = c->mode == KBZ_MODE_DYNAMORIO || (want & KBZ_WANT_H32) || a.x64 || h32_out;
+  a.h32 = !hashed ? nullptr : h32_out ? h32_out : c->h32;  // straight to the caller's buffer
+  c->cur_h32 = a.h32;
+  c->cur_h32_out = hashed ? h32_out : nullptr;
   a.neq = c->neq;
   a.chunk_or = c->chunk_or;
   a.chunk_cls = c->chunk_cls;
@@ -2163,7 +2422,7 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
     ev = &c->ev_pass1[c->ev_used_n++].first;
     HIP_TRY(hipEventRecord(ev[0], s));
   }
-  if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, s)) return -1;
+  if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, hashed, s)) return -1;
   if (ev) HIP_TRY(hipEventRecord(c->ev_pass1[c->ev_used_n - 1].second, s));
   if (c->mode == KBZ_MODE_DYNAMORIO) {  // the skip rule for rows j >= 1 needs no other shard
     const unsigned row_blocks = cdiv(n, 256);
@@ -2740,7 +2999,8 @@ int kbz_merge_and_host(uint8_t *out, const uint8_t *states, size_t n, size_t sta
 // ---- DynamoRIO per-module coverage ------------------------------------------------------------
 int kbz_triage_modules_device(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *traces, size_t n,
                               size_t stride, const size_t *module_offsets, const int8_t *outcome,
-                              uint8_t *hnb_out, uint8_t *any_out, void *stream) {
+                              uint8_t *hnb_out, uint8_t *any_out, uint32_t *h32_out,
+                              void *stream) {
   if (!ctxs || (k && !module_offsets) || (n && !hnb_out)) return fail("null argument");
   for (size_t m = 0; m < k; m++) {
     if (!ctxs[m]) return fail("kbz_triage_modules_device: null context");
@@ -2750,7 +3010,8 @@ int kbz_triage_modules_device(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *t
   }
   for (size_t m = 0; m < k; m++)
     if (kbz_triage_batch_device(ctxs[m], traces + module_offsets[m], n, stride, outcome,
-                                hnb_out + m * n, nullptr, nullptr, KBZ_WANT_H32, stream))
+                                hnb_out + m * n, h32_out ? h32_out + m * n : nullptr, nullptr,
+                                KBZ_WANT_H32, stream))
       return -1;
   if (any_out && n) {
     hipStream_t s = (hipStream_t)stream;
@@ -2766,7 +3027,7 @@ int kbz_triage_modules_device(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *t
 
 int kbz_triage_modules_host(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *traces, size_t n,
                             size_t stride, const size_t *module_offsets, const int8_t *outcome,
-                            uint8_t *hnb_out, uint8_t *any_out) {
+                            uint8_t *hnb_out, uint8_t *any_out, uint32_t *h32_out) {
   if (!ctxs || !k || !ctxs[0]) return fail("kbz_triage_modules_host: no modules");
   if (n && (!traces || !hnb_out)) return fail("null argument");
   if (stride & 15) return fail("kbz_triage_modules_host: stride must be a multiple of 16");
@@ -2774,11 +3035,13 @@ int kbz_triage_modules_host(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *tra
   DevGuard g(ctxs[0]->device);
   hipStream_t s = nullptr;
   uint8_t *d_t = nullptr, *d_hnb = nullptr, *d_any = nullptr;
+  uint32_t *d_h32 = nullptr;
   int8_t *d_oc = nullptr;
   int rc = -1;
   auto release = [&]() {
     (void)hipStreamSynchronize(s);
     if (d_t) (void)hipFree(d_t);
+    if (d_h32) (void)hipFree(d_h32);
     if (d_oc) (void)hipFree(d_oc);
     if (d_hnb) (void)hipFree(d_hnb);
     if (d_any) (void)hipFree(d_any);
@@ -2789,6 +3052,7 @@ int kbz_triage_modules_host(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *tra
         hipMalloc((void **)&d_t, n * stride) != hipSuccess ||
         hipMalloc((void **)&d_hnb, k * n) != hipSuccess ||
         hipMalloc((void **)&d_any, n) != hipSuccess ||
+        (h32_out && hipMalloc((void **)&d_h32, k * n * sizeof(uint32_t)) != hipSuccess) ||
         (outcome && hipMalloc((void **)&d_oc, n) != hipSuccess)) {
       fail("kbz_triage_modules_host: device staging");
       break;
@@ -2798,9 +3062,12 @@ int kbz_triage_modules_host(kbz_ctx_t *const *ctxs, size_t k, const uint8_t *tra
       fail("kbz_triage_modules_host: copy in");
       break;
     }
-    if (kbz_triage_modules_device(ctxs, k, d_t, n, stride, module_offsets, d_oc, d_hnb, d_any, s))
+    if (kbz_triage_modules_device(ctxs, k, d_t, n, stride, module_offsets, d_oc, d_hnb, d_any,
+                                  d_h32, s))
       break;
     if (hipMemcpyAsync(hnb_out, d_hnb, k * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        (h32_out && hipMemcpyAsync(h32_out, d_h32, k * n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   s) != hipSuccess) ||
         (any_out && hipMemcpyAsync(any_out, d_any, n, hipMemcpyDeviceToHost, s) != hipSuccess)) {
       fail("kbz_triage_modules_host: copy out");
       break;
@@ -2835,6 +3102,45 @@ int kbz_picker_ignore_device(const uint8_t *runs, size_t files, size_t iters, si
                      (uint32_t *)ignore_out, size / 4, (unsigned long long *)total_out);
   HIP_TRY(hipGetLastError());
   return 0;
+}
+
+int kbz_transform_rows_device(const uint8_t *rows, size_t n, size_t stride, size_t len, int xf,
+                              uint8_t *out, size_t out_stride, void *stream) {
+  if (xf < KBZ_XF_RAW || xf > KBZ_XF_SIMPLIFY) return fail("bad transform");
+  if ((len & 15) || (stride & 15) || (out_stride & 15) || ((uintptr_t)rows & 15) ||
+      ((uintptr_t)out & 15) || stride < len || out_stride < len)
+    return fail("kbz_transform_rows: len, strides and pointers must be 16-byte multiples/aligned");
+  if (!n || !len) return 0;
+  if (!rows || !out) return fail("null argument");
+  hipLaunchKernelGGL(k_transform_rows, dim3(cdiv(len / 16, 256), (unsigned)std::min<size_t>(n, 65535)),
+                     dim3(256), 0, (hipStream_t)stream, rows, n, stride, len, xf, out, out_stride);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+int kbz_transform_rows_host(const uint8_t *rows, size_t n, size_t stride, size_t len, int xf,
+                            uint8_t *out, size_t out_stride) {
+  if (xf < KBZ_XF_RAW || xf > KBZ_XF_SIMPLIFY) return fail("bad transform");
+  if ((len & 15) || stride < len || out_stride < len)
+    return fail("kbz_transform_rows: len must be a multiple of 16, strides >= len");
+  if (!n || !len) return 0;
+  if (!rows || !out) return fail("null argument");
+  uint8_t *d = nullptr;
+  HIP_TRY(hipMalloc((void **)&d, n * len));
+  int rc = -1;
+  do {
+    if (hipMemcpy2D(d, len, rows, stride, len, n, hipMemcpyHostToDevice) != hipSuccess) {
+      fail("kbz_transform_rows_host: copy in");
+      break;
+    }
+    if (kbz_transform_rows_device(d, n, len, len, xf, d, len, nullptr)) break;
+    if (hipMemcpy2D(out, out_stride, d, len, len, n, hipMemcpyDeviceToHost) != hipSuccess) {
+      fail("kbz_transform_rows_host: copy out");
+      break;
+    }
+    rc = 0;
+  } while (0);
+  (void)hipFree(d);
+  return rc;
 }
 
 int kbz_hash32_device(const uint8_t *rows, size_t n, size_t stride, size_t len, uint32_t seed,

@@ -58,6 +58,12 @@ def lib():
             for fn, (res, args) in _FN.items():
                 f = getattr(L, f"kbz_{name}_{fn}")
                 f.restype, f.argtypes = res, args
+        L.kbz_dynamorio_gpu_get_module_info.restype = _i
+        L.kbz_dynamorio_gpu_get_module_info.argtypes = [_vp, _i, C.POINTER(_i),
+                                                        C.POINTER(C.c_char_p),
+                                                        C.POINTER(C.c_void_p), C.POINTER(_i)]
+        L.kbz_dynamorio_gpu_get_edges.restype = _vp
+        L.kbz_dynamorio_gpu_get_edges.argtypes = [_vp, _i]
         L.kbz_instrumentation_factory.restype = C.POINTER(VTable)
         L.kbz_instrumentation_factory.argtypes = [C.c_char_p]
         L.kbz_plugin_last_error.restype = C.c_char_p
@@ -122,6 +128,24 @@ class Plugin:
 
     def is_process_done(self) -> int:
         return int(self._f("is_process_done")(self.h))
+
+    def get_module_info(self, index: int, want_info: bool = True):
+        """dynamorio_gpu get_module_info (dynamorio_instrumentation.c:1541-1573) as the picker
+        calls it (picker/main.c:187): -> (rc, is_new, name, info uint8[size] copy or None)."""
+        is_new, name, info, size = C.c_int(-1), C.c_char_p(), C.c_void_p(), C.c_int(0)
+        rc = lib().kbz_dynamorio_gpu_get_module_info(
+            self.h, int(index), C.byref(is_new), C.byref(name),
+            C.byref(info) if want_info else None, C.byref(size))
+        if rc:
+            return rc, None, None, None
+        arr = None
+        if want_info and info.value:
+            arr = np.ctypeslib.as_array(C.cast(info, C.POINTER(C.c_uint8)),
+                                        shape=(size.value,)).copy()
+        return rc, is_new.value, name.value.decode(), arr
+
+    def get_edges(self, index: int = 0):
+        return lib().kbz_dynamorio_gpu_get_edges(self.h, int(index))
 
     # batched API
     def triage_batch(self, traces: np.ndarray, outcome=None, hashes: bool = True):

@@ -18,6 +18,7 @@ FUZZ_NONE, FUZZ_HANG, FUZZ_CRASH = 0, 1, 2
 WANT_H32, WANT_X64 = 1, 2
 MODES = {"afl": MODE_AFL, "dynamorio": MODE_DYNAMORIO, "afl_classify": MODE_AFL_CLASSIFY}
 PASS1_AUTO, PASS1_NARROW, PASS1_WIDE = 0, 1, 2
+XF_RAW, XF_CLASSIFY, XF_SIMPLIFY = 0, 1, 2
 PASS1 = {"auto": PASS1_AUTO, "narrow": PASS1_NARROW, "wide": PASS1_WIDE}
 
 
@@ -298,11 +299,12 @@ def merge_and_host(states: np.ndarray) -> np.ndarray:
     return out
 
 
-def triage_modules(ctxs, traces, offsets, outcome=None, stream=None):
+def triage_modules(ctxs, traces, offsets, outcome=None, stream=None, hashes=False):
     """DynamoRIO per-module coverage (has_new_coverage_per_module,
     dynamorio_instrumentation.c:1477-1493) over an ordered batch.  ctxs: one TriageContext per
     module; traces: CUDA uint8 [n, row_bytes] holding every module's map at offsets[m].
-    Returns (hnb [k, n] uint8 per module, any [n] uint8: OR over modules)."""
+    Returns (hnb [k, n] uint8 per module, any [n] uint8: OR over modules), plus h32 [k, n] int32
+    (each module's hash32 per exec) when `hashes`."""
     import torch
 
     n, k = traces.shape[0], len(ctxs)
@@ -310,6 +312,7 @@ def triage_modules(ctxs, traces, offsets, outcome=None, stream=None):
     offs = (C.c_size_t * max(k, 1))(*offsets)
     hnb = torch.empty((k, n), dtype=torch.uint8, device=traces.device)
     anyv = torch.empty(n, dtype=torch.uint8, device=traces.device)
+    h32 = torch.empty((k, n), dtype=torch.int32, device=traces.device) if hashes else None
     oct = None
     if outcome is not None:  # device int8, alive until the kernels on `stream` have read it
         oct = outcome.to(device=traces.device, dtype=torch.int8).contiguous()
@@ -320,8 +323,26 @@ def triage_modules(ctxs, traces, offsets, outcome=None, stream=None):
                                           n, traces.stride(0), offs, oc,
                                           C.c_void_p(hnb.data_ptr()) if n else None,
                                           C.c_void_p(anyv.data_ptr()) if n else None,
+                                          C.c_void_p(h32.data_ptr()) if (hashes and n) else None,
                                           _stream_handle(stream)), "kbz_triage_modules_device")
-    return hnb, anyv
+    return (hnb, anyv, h32) if hashes else (hnb, anyv)
+
+
+def transform_rows(rows, xf, out=None, stream=None):
+    """classify_counts (xf=XF_CLASSIFY, dynamorio_instrumentation.c:265-292) or simplify_trace
+    (XF_SIMPLIFY, afl_instrumentation.c:674-706) of every row of a CUDA uint8 [n, len] tensor
+    (len % 16 == 0) into out (default: a new tensor)."""
+    import torch
+
+    n, ln = rows.shape
+    if out is None:
+        out = torch.empty((n, ln), dtype=torch.uint8, device=rows.device)
+    check(lib().kbz_transform_rows_device(C.c_void_p(rows.data_ptr()) if n else None, n,
+                                          rows.stride(0) if n else ln, ln, int(xf),
+                                          C.c_void_p(out.data_ptr()) if n else None,
+                                          out.stride(0) if n else ln, _stream_handle(stream)),
+          "kbz_transform_rows_device")
+    return out
 
 
 def picker_ignore(runs, stream=None):

@@ -73,33 +73,37 @@ def check(mode, traces, oc, ignore=None, virgin=None, last=0, want=WANT_H32 | WA
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_sparse_64k_partial_chunk(gpu, mode):
+@pytest.mark.parametrize("want", [0, WANT_H32 | WANT_X64], ids=["nohash", "hashes"])
+def test_sparse_64k_partial_chunk(gpu, mode, want):
     t, oc = synth.sparse_np(1000, 65536, seed=100 + mode)
-    exp = check(mode, t, oc)
+    exp = check(mode, t, oc, want=want)
     assert exp["hnb"].max() == 2
 
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("density", [0.02, 0.3, 1.0])
-def test_uniform_density(gpu, mode, density):
+@pytest.mark.parametrize("want", [0, WANT_H32 | WANT_X64], ids=["nohash", "hashes"])
+def test_uniform_density(gpu, mode, density, want):
     t = synth.uniform_np(200, 65536, seed=int(density * 100), density=density)
     rng = np.random.default_rng(7)
     oc = rng.choice(3, size=200, p=[0.7, 0.15, 0.15]).astype(np.int8)
-    check(mode, t, oc)
+    check(mode, t, oc, want=want)
 
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("m", [256, 4096, 1 << 20])
-def test_map_sizes(gpu, mode, m):
+@pytest.mark.parametrize("want", [0, WANT_H32 | WANT_X64], ids=["nohash", "hashes"])
+def test_map_sizes(gpu, mode, m, want):
     t, oc = synth.sparse_np(130, m, seed=m + mode, hot_frac=0.05)
-    check(mode, t, oc)
+    check(mode, t, oc, want=want)
 
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("n", [0, 1, 63, 64, 65])
-def test_small_batches(gpu, mode, n):
+@pytest.mark.parametrize("want", [0, WANT_H32 | WANT_X64], ids=["nohash", "hashes"])
+def test_small_batches(gpu, mode, n, want):
     t, oc = synth.sparse_np(n, 4096, seed=n)
-    check(mode, t, oc)
+    check(mode, t, oc, want=want)
 
 
 def test_dynamorio_identical_runs_and_chunk_boundary(gpu):
@@ -140,7 +144,8 @@ def test_dynamorio_ignore_skips_that_differ(gpu):
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_preset_virgin_and_sequential_composition(gpu, mode):
+@pytest.mark.parametrize("want", [0, WANT_H32 | WANT_X64], ids=["nohash", "hashes"])
+def test_preset_virgin_and_sequential_composition(gpu, mode, want):
     m = 65536
     rng = np.random.default_rng(8)
     v = rng.integers(0, 256, size=(3, m)).astype(np.uint8)
@@ -150,16 +155,28 @@ def test_preset_virgin_and_sequential_composition(gpu, mode):
     ctx.set_virgin(v)
     # three uneven batches in a row == one sequential pass
     for lo, hi in ((0, 1), (1, 333), (333, 700)):
-        check(mode, t[lo:hi], oc[lo:hi], ctx=ctx)
+        check(mode, t[lo:hi], oc[lo:hi], ctx=ctx, want=want)
     whole = oracle.triage_batch(mode, t, oc, virgin=v)
     np.testing.assert_array_equal(ctx.get_virgin(), whole["virgin"])
     ctx.close()
 
 
 @pytest.mark.parametrize("mode", [MODE_AFL, MODE_AFL_CLASSIFY])
-def test_crash_hang_heavy(gpu, mode):
+@pytest.mark.parametrize("want", [0, WANT_H32 | WANT_X64], ids=["nohash", "hashes"])
+def test_crash_hang_heavy(gpu, mode, want):
     t, oc = synth.sparse_np(500, 65536, seed=12, outcome_p=(0.4, 0.3, 0.3))
-    check(mode, t, oc)
+    check(mode, t, oc, want=want)
+
+
+@pytest.mark.parametrize("mode", [MODE_AFL, MODE_AFL_CLASSIFY])
+@pytest.mark.parametrize("oc_all", [1, 2])
+def test_all_hang_or_crash_no_hash(gpu, mode, oc_all):
+    """Every exec a hang (or crash): only the simplified class is present (simplify_trace
+    afl_instrumentation.c:674-706), with all-zero rows (0x01 everywhere) in some chunks."""
+    t, _ = synth.sparse_np(700, 4096, seed=20 + oc_all, hot_frac=0.05)
+    t[64:70] = 0
+    t[300:364] = 0
+    check(mode, t, np.full(700, oc_all, np.int8), want=0)
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -468,7 +485,8 @@ N_AT_SCALE = 32768 + 37  # 513 chunks, the last one partial
 
 @pytest.mark.parametrize("mode", [MODE_AFL, MODE_AFL_CLASSIFY])
 @pytest.mark.parametrize("m", [256, 4096])
-def test_at_scale_afl_outcome_routing(gpu, mode, m):
+@pytest.mark.parametrize("want", [0, WANT_H32, WANT_H32 | WANT_X64], ids=["nohash", "h32", "h32x64"])
+def test_at_scale_afl_outcome_routing(gpu, mode, m, want):
     """3 virgin maps (finish_fuzz_round afl_instrumentation.c:231-274): 5 % hangs + crashes go
     simplified to virgin_tmout / virgin_crash, with all-zero traces (simplify's 0x01 words) and
     identical neighbours; XXH64 on; a second batch carries the three maps."""
@@ -478,12 +496,12 @@ def test_at_scale_afl_outcome_routing(gpu, mode, m):
     t[640:700] = t[639]
     oc[640:700] = oracle.FUZZ_CRASH
     ctx = TriageContext(m, mode, N_AT_SCALE)
-    e1 = check(mode, t, oc, ctx=ctx)
+    e1 = check(mode, t, oc, ctx=ctx, want=want)
     for k in range(3):
         assert (e1["hnb"][oc == k] > 0).any()
     t2, oc2 = synth.sparse_np(N_AT_SCALE, m, seed=232 + m + mode, hot_frac=0.05,
                               outcome_p=(0.9, 0.05, 0.05))
-    check(mode, t2, oc2, ctx=ctx)
+    check(mode, t2, oc2, ctx=ctx, want=want)
     ctx.close()
 
 
@@ -626,12 +644,13 @@ def test_abandoned_batch_is_rearmed(gpu, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_config3_dense_1m(gpu, mode):
+@pytest.mark.parametrize("want", [0, WANT_H32 | WANT_X64], ids=["nohash", "hashes"])
+def test_config3_dense_1m(gpu, mode, want):
     """BASELINE config 3's traces (dense: 50 % hot, counts U[1,255]) at 1 MiB, at a batch size
     the sequential oracle checks in seconds, crash/hang mixed in."""
     t, oc = synth.dense_np(300, 1 << 20, seed=3 + mode, outcome_p=(0.8, 0.1, 0.1))
     t[65] = t[64]
-    check(mode, t, oc)
+    check(mode, t, oc, want=want)
 
 
 @pytest.mark.slow

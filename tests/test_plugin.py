@@ -38,7 +38,11 @@ def test_factory_vtable_order():
                        "enable", "is_new_path", "get_fuzz_result", "is_process_done",
                        "triage_batch", "merge_many"):
             assert getattr(v, member) == _fn_addr(f"kbz_{name}_{member}"), (name, member)
-        assert v.get_module_info is None and v.get_edges is None
+        if name == "afl_gpu":  # the afl plugin binds neither (instrumentation_factory.c:72-84)
+            assert v.get_module_info is None and v.get_edges is None
+        else:                  # dynamorio binds both (instrumentation_factory.c:53-54)
+            assert v.get_module_info == _fn_addr("kbz_dynamorio_gpu_get_module_info")
+            assert v.get_edges == _fn_addr("kbz_dynamorio_gpu_get_edges")
         C.CDLL(None).free(vt)
     assert not L.kbz_instrumentation_factory(b"afl")
 
@@ -70,6 +74,48 @@ def test_state_roundtrip_without_gpu(name):
     assert q.is_process_done() == -1
     assert q.set_state('{"map_size": 8192}') != 0
     assert q.set_state('{"virgin_bits": "zz"}') != 0
+
+
+def test_dynamorio_state_keeps_last_process_status():
+    """dynamorio_set_state restores last_process_status (:1325); get_state reports it until the
+    next exec (a get -> set -> get round trip keeps it)."""
+    opts = f'{{"map_size": {M}}}'
+    st = P.state_json({"virgin_bits": np.full(M, 0xFF, np.uint8), "last_shm_hash": 7,
+                       "last_path_was_new": 1, "last_process_status": P.FUZZ_CRASH}, M)
+    p = P.Plugin("dynamorio_gpu", opts, st)
+    back = P.state_maps(p.get_state(), M)
+    assert back["last_process_status"] == P.FUZZ_CRASH and back["last_shm_hash"] == 7
+    q = P.Plugin("dynamorio_gpu", opts, p.get_state())
+    assert P.state_maps(q.get_state(), M)["last_process_status"] == P.FUZZ_CRASH
+    assert q.get_fuzz_result() == P.FUZZ_ERROR  # no exec yet (the reference: enable not called)
+    assert q.set_state(st.replace('"last_process_status": 2', '"last_process_status": -1')) != 0
+
+
+def test_state_keys_are_top_level_only():
+    """A key inside a nested object must not be taken for the top-level one: a per-module state's
+    module objects repeat virgin_bits / last_shm_hash (dynamorio_get_state :1260-1275)."""
+    v = np.full(M, 0xFF, np.uint8)
+    v[3] = 0x12
+    inner = bytes(np.zeros(M, np.uint8)).hex()
+    st = ('{"map_size": %d, "decoy": {"virgin_bits": "%s", "last_shm_hash": 99}, '
+          '"last_process_status": 0, "last_path_was_new": 0, "last_shm_hash": 5, '
+          '"virgin_bits": "%s"}') % (M, inner, bytes(v).hex())
+    p = P.Plugin("dynamorio_gpu", f'{{"map_size": {M}}}', st)
+    back = P.state_maps(p.get_state(), M)
+    np.testing.assert_array_equal(back["virgin_bits"], v)
+    assert back["last_shm_hash"] == 5
+    # a top-level key missing while a nested one exists: rejected, not read from the nest
+    bad = '{"map_size": %d, "x": {"virgin_bits": "%s"}}' % (M, inner)
+    assert p.set_state(bad) != 0
+    # escapes in strings are decoded (module names), malformed text is an error
+    opts = ('{"map_size": %d, "per_module_coverage": 1, "coverage_modules": ["a\\u00e9\\"b", '
+            '"c"]}' % M)
+    q = P.Plugin("dynamorio_gpu", opts)
+    assert P.state_maps(q.get_state(), M)["modules"].keys() == {'a\u00e9"b', "c"}
+    for broken in ('{"map_size": %d' % M, '{"map_size": -1}', '{"map_size": 4096,}',
+                   '{"virgin_bits": "ff" "x"}', '[1, 2]', '{"a": [1, {"b": }]}', '',
+                   '{"map_size": 99999999999999999999999}'):
+        assert p.set_state(broken) != 0, broken
 
 
 def test_bad_options_and_ignore_file(tmp_path):
