@@ -2235,6 +2235,9 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
                : !strcmp(force, "narrow") ? KBZ_PASS1_NARROW : KBZ_PASS1_AUTO;
   const size_t M = map_size, nc = c->nc;
   c->item_cap = (uint32_t)std::min<size_t>(kItemsPerCol * M * nc + 1024, 0xffffffffu);
+  // tests only: a smaller claim list, to exercise the overflow error path (a real batch cannot
+  // overflow it: each column yields at most 8 items per map per batch)
+  if (const char *cap = getenv("KBZ_DEBUG_ITEM_CAP")) c->item_cap = std::max(1, atoi(cap));
   bool ok = !dalloc(&c->V[0], 3 * M) && !dalloc(&c->V[1], 3 * M) && !dalloc(&c->last, 2) &&
             !dalloc(&c->chunk_or, c->max_chunks * nc * M) && !dalloc(&c->chunk_cls, c->max_chunks) &&
             !dalloc(&c->tflags, c->max_chunks * nc * c->nfw) &&
@@ -2283,10 +2286,12 @@ int kbz_set_ignore(kbz_ctx_t *c, const uint8_t *host_ignore) {
   if (!host_ignore) {
     if (c->ignore) (void)hipFree(c->ignore);
     c->ignore = nullptr;
+    c->saved_valid = false;
     return 0;
   }
   if (!c->ignore && dalloc(&c->ignore, c->M)) return -1;
   HIP_TRY(hipMemcpy(c->ignore, host_ignore, c->M, hipMemcpyHostToDevice));
+  c->saved_valid = false;  // "same content as the last exec" depended on the examined bytes
   return 0;
 }
 
@@ -2302,6 +2307,9 @@ int kbz_set_virgin(kbz_ctx_t *c, const uint8_t *in) {
   DevGuard g(c->device);
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(c->V[c->vcur], in, 3 * c->M, hipMemcpyHostToDevice));
+  // the saved last row's "clean" flag said its bits were in V; with new maps they may not be,
+  // so a repeat of it in the next batch is checked like one after a restored hash
+  c->saved_valid = false;
   return 0;
 }
 int kbz_get_last_hash(kbz_ctx_t *c, uint32_t *out) {
@@ -2368,6 +2376,9 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
     HIP_TRY(hipMemsetAsync(c->shard_last, 0, 2 * sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(c->hnb32, 0, c->max_batch * sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(c->segor, 0, kMaxSeg * c->nc * c->M, s));
+    // kbz_shard_link may already have marked this batch's last row as the next row-0
+    // predecessor, but V never received that batch: forget the row
+    c->saved_valid = false;
     c->stage = 0;
   }
   c->cur_traces = traces;
@@ -2637,8 +2648,10 @@ int kbz_sync(kbz_ctx_t *c, void *stream) {
 #endif
   if (cnt[1] || cnt[2]) {  // sticky until reported here
     HIP_TRY(hipMemset(c->counters + 1, 0, 2 * sizeof(uint32_t)));
+    c->h_err[0] = c->h_err[1] = 0;  // k_pack's host-mapped copy: reported now, not again
     return fail(cnt[1] ? "claim list overflow" : "inconsistent claim (internal error)");
   }
+  c->h_err[0] = c->h_err[1] = 0;
   return 0;
 }
 
@@ -2781,11 +2794,14 @@ int kbz_ring_acquire(kbz_ctx_t *c, uint8_t **rows, int8_t **outcome, size_t *cap
   const int sl = c->ring_next;
   HIP_TRY(hipEventSynchronize(c->ev_used[sl]));  // its previous batch is done
   ring_deliver(c->ring[sl]);
+  // an error of an earlier batch is reported (once) with no slot handed out, so the caller's
+  // next acquire starts clean instead of finding a slot it never received still held
+  if (ring_errors(c)) return -1;
   c->ring_acquired = sl;
   *rows = c->pin[sl];
   if (outcome) *outcome = c->pin_oc[sl];
   if (cap) *cap = c->slot_rows;
-  return ring_errors(c);
+  return 0;
 }
 
 // Batches of at most one chunk are triaged straight from the pinned slot and write their

@@ -179,6 +179,19 @@ def triage_batch(mode, traces, outcome=None, virgin=None, ignore=None, last_hash
     return dict(hnb=hnb, h32=h32, x64=x64, virgin=v, last_hash=lh.value)
 
 
+def transform(traces: np.ndarray, xf: int) -> np.ndarray:
+    """classify_counts (xf=1, dynamorio_instrumentation.c:265-292) or simplify_trace (xf=2,
+    afl_instrumentation.c:674-706) of every row (restated; returns a transformed copy)."""
+    t = np.array(traces, np.uint8, copy=True)
+    if xf == 0:
+        return t
+    f = lib().kbzo_classify_counts if xf == 1 else lib().kbzo_simplify_trace
+    flat = t.reshape(-1, t.shape[-1])
+    for row in flat:
+        f(_p(row), row.size)
+    return t
+
+
 def merge_many(states: np.ndarray) -> np.ndarray:
     s = np.ascontiguousarray(states, dtype=np.uint8)
     n = s.shape[0]

@@ -677,3 +677,63 @@ def test_full_size_config3(gpu):
     assert int(out2["hnb"].max()) == 0
     np.testing.assert_array_equal(ctx.get_virgin(), v)
     ctx.close()
+
+
+@pytest.mark.parametrize("xf", [0, 1, 2])
+def test_transform_rows(gpu, xf):
+    """kbz_transform_rows_device: classify_counts / simplify_trace of every row (the maps
+    get_module_info and dump_map_dir hand out), strided rows, against the restatement."""
+    import torch
+
+    from killerbeez_amd.triage import transform_rows
+
+    t = synth.uniform_np(300, 4096, seed=xf, density=0.3)
+    t[5] = 0
+    big = torch.zeros((300, 4096 + 256), dtype=torch.uint8, device="cuda")
+    big[:, :4096] = torch.from_numpy(t).cuda()
+    got = transform_rows(big[:, :4096], xf)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy(), oracle.transform(t, xf))
+
+
+def test_set_virgin_after_a_batch_forgets_the_saved_row(gpu):
+    """A batch ends in row R; the virgin maps are then replaced (kbz_set_virgin) with the last
+    hash kept; the next batch starts with R again (a last-hash skip: never applied) and then a
+    row holding R's edges, which is new against the fresh maps.  The saved row may no longer
+    be taken as already absorbed."""
+    m = 4096
+    t, oc = synth.sparse_np(200, m, seed=2045, hot_frac=0.05)
+    ctx = TriageContext(m, MODE_DYNAMORIO, 200)
+    check(MODE_DYNAMORIO, t[:100], oc[:100], ctx=ctx)
+    fresh = np.full((3, m), 0xFF, np.uint8)
+    ctx.set_virgin(fresh)
+    t2 = t[100:].copy()
+    t2[0] = t[99]
+    t2[1] = t[99]
+    t2[1, 7] ^= 0x01                                  # R's edges plus a changed byte
+    exp = check(MODE_DYNAMORIO, t2, oc[100:], ctx=ctx)
+    assert exp["hnb"][0] == 0 and exp["hnb"][1] == 2
+    ctx.close()
+
+
+def test_claim_overflow_is_reported_once(gpu, monkeypatch):
+    """A claim-list overflow (forced with a tiny debug list) fails that batch once: the next
+    ring acquire / record works and later batches are exact again."""
+    from killerbeez_amd import plugin as P
+
+    monkeypatch.setenv("KBZ_DEBUG_ITEM_CAP", "16")
+    m = 4096
+    t, oc = synth.sparse_np(300, m, seed=2529, hot_frac=0.05)
+    p = P.Plugin("afl_gpu", '{"map_size": %d, "max_batch": 256}' % m)
+    with pytest.raises(RuntimeError, match="overflow"):
+        p.triage_batch(t[:200], oc[:200])            # fresh maps: far more than 16 claims
+    v = P.state_maps(p.get_state(), m)
+    vm = np.stack([v["virgin_bits"], v["virgin_tmout"], v["virgin_crash"]])
+    one = np.zeros((1, m), np.uint8)
+    one[0, 11] = 3                                   # a new edge: a handful of claims
+    for j, row in enumerate([t[200], one[0], t[201]]):
+        tk = p.record(row, P.FUZZ_NONE)
+        assert tk >= 0, P.last_error()
+        rows = np.stack([t[200], one[0], t[201]])[:j + 1]
+        exp = oracle.triage_batch(MODE_AFL, rows, np.zeros(j + 1, np.int8), virgin=vm)
+        assert p.result(tk) == exp["hnb"][j]

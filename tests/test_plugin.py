@@ -408,3 +408,111 @@ def test_per_module_coverage_plugin(gpu, tmp_path):
         np.testing.assert_array_equal(got[name]["virgin_bits"],
                                       exp[i]["virgin"][0] & exp2[i]["virgin"][0])
         assert got[name]["last_shm_hash"] == 0
+
+
+# ---- get_module_info / get_edges / dump_map_dir (dynamorio_instrumentation.c:1541-1606, :1453) --
+
+@pytest.mark.gpu
+def test_get_module_info_like_the_picker(gpu):
+    """picker/main.c:182-225 drives the plugin: per input file and iteration, test_input (here:
+    record the exec's module maps) then get_module_info(index) for index = 0, 1, ... until it
+    fails, collecting each module's is_new and trace map.  The maps must be the classified maps
+    has_new_coverage leaves in trace_bits (:1434, :1565), is_new the module's has_new_coverage
+    result for that exec; the collected maps then feed the picker's diff on the GPU
+    (kbz_picker_ignore_device), checked against the restated picker loop."""
+    import json
+
+    import torch
+
+    from killerbeez_amd.triage import picker_ignore
+
+    files, iters, k = 3, 5, len(MODS)
+    rng = np.random.default_rng(187)
+    p = P.Plugin("dynamorio_gpu", PM_OPTS % (M, json.dumps(MODS)))
+    assert p.get_module_info(0)[0] == -1          # no exec yet (enable_called)
+    base = [[synth.sparse_np(1, M, seed=100 * f + i, hot_frac=0.05)[0][0] for i in range(k)]
+            for f in range(files)]
+    collected = np.zeros((k, files, iters, M), np.uint8)
+    is_new = np.zeros((k, files * iters), np.int64)
+    rows = []
+    for f in range(files):
+        for it in range(iters):
+            maps = [b.copy() for b in base[f]]
+            if it % 2:                              # module 1 is noisy on odd iterations
+                maps[1][rng.choice(M, 3, replace=False)] = rng.integers(1, 256, 3)
+            row = np.concatenate(maps)
+            rows.append(row)
+            assert p.record(row, P.FUZZ_NONE) >= 0  # driver->test_input
+            index = 0
+            while True:
+                rc, nw, name, info = p.get_module_info(index)
+                if rc:
+                    assert rc == 1
+                    break
+                assert name == MODS[index] and info.size == M
+                collected[index, f, it] = info
+                is_new[index, f * iters + it] = nw
+                index += 1
+            assert index == k
+    raw = np.array(rows)
+    for i in range(k):
+        part = raw[:, i * M:(i + 1) * M]
+        exp = oracle.triage_batch(oracle.MODE_DYNAMORIO, part, None)
+        np.testing.assert_array_equal(collected[i].reshape(-1, M), oracle.transform(part, 1))
+        np.testing.assert_array_equal(is_new[i], (exp["hnb"] != 0).astype(np.int64))
+        g_ign, g_pc, g_tot = picker_ignore(torch.from_numpy(collected[i]).cuda())
+        torch.cuda.synchronize()
+        ign, pc, tot = oracle.picker_ignore(collected[i])
+        np.testing.assert_array_equal(g_ign.cpu().numpy(), ign)
+        np.testing.assert_array_equal(g_pc.cpu().numpy().view(np.uint32), pc)
+        assert int(g_tot.item()) == tot
+        assert (tot > 0) == (i == 1)                # only the noisy module has ignore bytes
+    assert p.get_edges(0) is None                   # no edge lists without the edges option
+    # without per_module_coverage the coverage modules are named, without maps (as the reference)
+    q = P.Plugin("dynamorio_gpu", '{"map_size": %d, "coverage_modules": ["t.exe"]}' % M)
+    q.record(raw[0, :M], P.FUZZ_NONE)
+    assert q.get_module_info(0) == (0, 0, "t.exe", None)
+    assert q.get_module_info(1)[0] == 1
+
+
+def _golden_config1(tag):
+    f = np.load(os.path.join(os.path.dirname(__file__), "golden", "config1.npz"))
+    n = int(f[f"{tag}_n"])
+    t = np.zeros((n, 65536), np.uint8)
+    t[f[f"{tag}_tj"], f[f"{tag}_ti"]] = f[f"{tag}_tv"]
+    return t, f[f"{tag}_outcome"], f[f"{tag}_dynamorio_h32"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["record", "triage_batch"])
+def test_dump_map_dir_config1(gpu, tmp_path, path):
+    """dump_map_dir (dynamorio_instrumentation.c:1453-1458) on BASELINE config 1's real traces:
+    every exec whose hash32 differs from the previous exec's writes its classified map to
+    <dir>/<%08x hash>.  File names come from the reference build's own hashes (config1.npz),
+    contents from the restated classify_counts."""
+    import json
+
+    t, oc, ref_h32 = _golden_config1("aaaa")
+    t, oc, ref_h32 = t[:300], oc[:300], ref_h32[:300]
+    d = tmp_path / "maps"
+    d.mkdir()
+    p = P.Plugin("dynamorio_gpu", json.dumps({"map_size": 65536, "max_batch": 64,
+                                              "dump_map_dir": str(d)}))
+    if path == "record":
+        for j in range(t.shape[0]):
+            p.record(t[j], int(oc[j]))
+            if j % 37 == 0:
+                assert p.is_new_path() >= 0         # flush windows of varying size
+        assert p.flush() == 0
+    else:
+        p.triage_batch(t, oc, hashes=False)
+    want, prev = {}, 0
+    classified = oracle.transform(t, 1)
+    for j, h in enumerate(ref_h32.tolist()):
+        if h != prev:
+            want[f"{h:08x}"] = classified[j]
+        prev = h
+    got = {x.name: np.frombuffer(x.read_bytes(), np.uint8) for x in d.iterdir()}
+    assert set(got) == set(want) and len(want) > 1
+    for name, m in want.items():
+        np.testing.assert_array_equal(got[name], m)
