@@ -341,7 +341,7 @@ def main_triage(args):
     import torch
 
     from killerbeez_amd import synth
-    from killerbeez_amd.dist import triage_sharded
+    from killerbeez_amd.dist import timing_summary, triage_sharded
     from killerbeez_amd.triage import MODES, WANT_H32, TriageContext
 
     world, rank, dev = init_dist()
@@ -362,6 +362,7 @@ def main_triage(args):
     if want:
         out["h32"] = torch.empty(B, dtype=torch.int32, device=dev)
     counts = [B] * world
+    phase_log = None  # list: per-batch phase timings of the sharded protocol (world > 1)
 
     def step(t, oc):
         if world == 1:
@@ -370,7 +371,7 @@ def main_triage(args):
             ctx.shard_reduce()
             ctx.shard_finish(None, None)  # single shard: its own aggregate is the total
         else:
-            triage_sharded(ctx, t, oc, counts, rank, world, want, device=dev)
+            triage_sharded(ctx, t, oc, counts, rank, world, want, device=dev, timings=phase_log)
 
     def timed(batches, k, events=False):
         """k steps over batches[i % len], bracketed by barrier + synchronize; max over ranks.
@@ -396,7 +397,10 @@ def main_triage(args):
     for i in range(1, args.warmup):
         step(*pool[i % npool])
     fresh = pool[args.warmup:] if npool > args.warmup else pool
+    phase_log = [] if world > 1 else None
     elapsed, pass1_ms = timed(fresh, args.steps)
+    phases = timing_summary(phase_log) if phase_log else {}
+    phase_log = None
     n_fresh = min(args.steps, len(fresh))
     fresh_stats = ctx.stats()  # work of the last timed batch (claim items resolved, ...)
     value = world * B * args.steps / elapsed
@@ -472,6 +476,24 @@ def main_triage(args):
         "pass1_share_of_step": round(pass1_ms / ms_per_step, 4),
         "variants": variants,
     }
+    if world > 1:
+        # attribution of a sub-linear curve: every rank's pass-1 time and the time its steps
+        # spent in the all-gathers (HIP events around each phase of the timed steps)
+        import torch.distributed as dist
+
+        mine = torch.tensor([pass1_ms, phases.get("collective", 0.0), phases.get("pass1", 0.0)],
+                            dtype=torch.float64, device=dev)
+        allv = torch.empty(world * 3, dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(allv, mine)
+        allv = allv.view(world, 3).cpu().tolist()
+        res["per_rank_pass1_ms"] = [round(v[0], 4) for v in allv]
+        res["collective_ms"] = {"max_over_ranks": round(max(v[1] for v in allv), 4),
+                                "per_rank": [round(v[1], 4) for v in allv],
+                                "what": "mean per step of the rank's all-gathers (DynamoRIO "
+                                        "last row + hash, aggregates), HIP events"}
+        res["phase_ms_rank0"] = {k: round(v, 4) for k, v in phases.items()}
+        res["rccl_world"] = {"world_size": world, "backend": dist.get_backend(),
+                             "rehearsal_one_gpu": REHEARSE}
     if rank == 0 and world == 1 and not args.no_cpu:
         t0, oc0 = gen(min(B, 16384), M, seed=args.seed + 1, device=dev, hot_seed=args.seed)
         res["cpu_baseline"] = cpu_baseline(t0, oc0, mode, args.cpu_seconds)
@@ -650,6 +672,9 @@ def main_stream(args):
     barrier_sync(world, dev)
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
     traces = world * slot * args.steps
+    pcie = pcie_h2d_peak(dev)
+    gbps = slot * M * args.steps / el / 1e9
+    ins = table_insert_rate(dev)
     res = {"metric": "traces triaged/sec from host memory (64KB map, PCIe-inclusive) + unique "
                      "crash/hang table",
            "value": round(traces / el, 1), "unit": "traces/s", "n_gpus": world,
@@ -661,12 +686,60 @@ def main_stream(args):
                                   "pinned ring, XXH64 keys of crash/hang traces into the "
                                   "replicated unique table", "slot": slot, "map_size": M,
                       "mode": args.mode, "parallelism": f"shard{world}"},
-           "pcie_GBps_per_gpu": round(slot * M * args.steps / el / 1e9, 2),
+           "pcie_GBps_per_gpu": round(gbps, 2),
+           "pcie_h2d_peak_GBps": pcie,
+           "pcie_frac": round(gbps / pcie["value"], 4),
+           "xxh64_table_insert": ins,
            "unique_crash_hang_keys": table.size(), "new_keys_reported": n_new}
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()
     finish(world)
+
+
+def pcie_h2d_peak(dev, mib=256, reps=8):
+    """SURVEY.md §8(d) row 5's ceiling, measured in the same run: a pinned-host -> HBM
+    hipMemcpyAsync of `mib` MiB, best of `reps` (HIP events on the copy's stream)."""
+    import torch
+
+    n = mib << 20
+    src = torch.empty(n, dtype=torch.uint8).pin_memory()
+    dst = torch.empty(n, dtype=torch.uint8, device=dev)
+    best = float("inf")
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        dst.copy_(src, non_blocking=True)
+        b.record()
+        b.synchronize()
+        best = min(best, a.elapsed_time(b))
+    return {"value": round(n / (best * 1e-3) / 1e9, 2), "unit": "GB/s",
+            "what": f"pinned {mib} MiB hipMemcpyAsync H2D, best of {reps}"}
+
+
+def table_insert_rate(dev, n=1 << 20, batches=8):
+    """Inserts/s of the unique crash/hang table (kbz_set_insert_device, ordered insert-if-absent)
+    for batches of n random keys into a set sized for all of them (device-resident keys)."""
+    import torch
+
+    from killerbeez_amd.triage import UniqueSet
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    keys = [torch.randint(-2**62, 2**62, (n, 2), dtype=torch.int64, device=dev, generator=g)
+            for _ in range(batches)]
+    table = UniqueSet(n * batches)
+    table.insert(keys[0][:1024])  # warm
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for k in keys:
+        table.insert(k)
+    b.record()
+    b.synchronize()
+    ms = a.elapsed_time(b)
+    return {"value": round(n * batches / (ms * 1e-3), 1), "unit": "keys/s",
+            "what": f"{batches} ordered batches of {n} random 16-B keys into one table"}
 
 
 # ---- plugin per-exec latency -------------------------------------------------------------------

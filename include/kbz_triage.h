@@ -199,6 +199,10 @@ int kbz_shard_finish(kbz_ctx_t *ctx, const uint8_t *prefix, const uint8_t *total
 /* out[i] = OR of in[r*bytes + i] for r in [r_lo, r_hi).  Device, stream-ordered. */
 int kbz_or_reduce(uint8_t *out, const uint8_t *in, size_t r_lo, size_t r_hi, size_t bytes,
                   void *stream);
+/* Step 4 in one launch: prefix_out = OR of ranks [0, rank) (NULL: not wanted), total_out = OR of
+ * all `world` rows of the all-gathered aggregates `in` (world x bytes).  Device, stream-ordered. */
+int kbz_or_prefix_total(uint8_t *prefix_out, uint8_t *total_out, const uint8_t *in, size_t rank,
+                        size_t world, size_t bytes, void *stream);
 
 /* ---- merger -------------------------------------------------------------------------------- */
 /* out = AND of n states (state_bytes each, typically 3*map_size), row s at states +

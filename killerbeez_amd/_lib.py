@@ -44,6 +44,7 @@ SIGNATURES = [
     ("kbz_shard_aggregate_bytes", _sz, [_vp]),
     ("kbz_shard_finish", _i, [_vp, _vp, _vp, _vp, _vp]),
     ("kbz_or_reduce", _i, [_vp, _vp, _sz, _sz, _sz, _vp]),
+    ("kbz_or_prefix_total", _i, [_vp, _vp, _vp, _sz, _sz, _sz, _vp]),
     ("kbz_merge_and_device", _i, [_vp, _vp, _sz, _sz, _vp]),
     ("kbz_merge_and_host", _i, [_vp, _vp, _sz, _sz]),
     ("kbz_merge_and_fill", _i, [_vp, _sz, _sz, _vp, _vp]),

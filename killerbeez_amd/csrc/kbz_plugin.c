@@ -930,7 +930,7 @@ static char *plugin_get_state(kbz_plugin_t *p) {
   if (plugin_flush(p) || sync_mirror(p)) return NULL;
   const size_t m = p->map_size, k = p->per_module ? p->nmod : nmaps(p);
   size_t extra = 0;
-  for (size_t i = 0; p->per_module && i < p->nmod; i++) extra += 2 * strlen(p->mod_names[i]) + 128;
+  for (size_t i = 0; p->per_module && i < p->nmod; i++) extra += 6 * strlen(p->mod_names[i]) + 128;
   char *s = (char *)malloc(256 + k * (2 * m + 64) + extra);
   if (!s) {
     set_err("out of host memory");
@@ -945,7 +945,11 @@ static char *plugin_get_state(kbz_plugin_t *p) {
     o += sprintf(o, ",\"modules\":[");
     for (size_t i = 0; i < p->nmod; i++) {
       o += sprintf(o, "%s{\"name\":\"", i ? "," : "");
-      for (const char *c = p->mod_names[i]; *c; c++) {
+      for (const char *c = p->mod_names[i]; *c; c++) {  /* JSON string escapes */
+        if ((unsigned char)*c < 0x20) {
+          o += sprintf(o, "\\u%04x", (unsigned char)*c);
+          continue;
+        }
         if (*c == '"' || *c == '\\') *o++ = '\\';
         *o++ = *c;
       }
@@ -1038,8 +1042,9 @@ static int plugin_set_state(kbz_plugin_t *p, const char *json) {
     return 1;
   }
   unsigned long long m = 0, h = 0, lw = 0, ls = 0;
-  if (json_u64(json, "map_size", &m) == 1 && m != p->map_size) {
-    set_err("state map_size %llu does not match the plugin's %zu", m, p->map_size);
+  const int hm = json_u64(json, "map_size", &m);
+  if (hm < 0 || (hm == 1 && m != p->map_size)) {
+    set_err("state map_size does not match the plugin's %zu", p->map_size);
     return 1;
   }
   /* execs recorded before the new state was loaded belong to the old one */

@@ -1749,6 +1749,33 @@ __global__ __launch_bounds__(256) void k_or_reduce(uint8_t *out, const uint8_t *
   }
 }
 
+// The sharded protocol's prefix (OR of ranks < rank) and total (OR of all ranks) of the
+// all-gathered aggregates, in one pass over them (16 B per thread; prefix may be null).
+__global__ __launch_bounds__(256) void k_or_prefix_total(uint8_t *prefix, uint8_t *total,
+                                                          const uint8_t *in, size_t rank,
+                                                          size_t world, size_t bytes) {
+  const size_t i = (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (i + 16 <= bytes) {
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (size_t r = 0; r < world; r++) {
+      if (r == rank && prefix) *(uint4 *)(prefix + i) = acc;
+      acc = or4(acc, *(const uint4 *)(in + r * bytes + i));
+    }
+    if (rank >= world && prefix) *(uint4 *)(prefix + i) = acc;
+    *(uint4 *)(total + i) = acc;
+  } else {
+    for (size_t b = i; b < bytes; b++) {
+      uint8_t acc = 0;
+      for (size_t r = 0; r < world; r++) {
+        if (r == rank && prefix) prefix[b] = acc;
+        acc |= in[r * bytes + b];
+      }
+      if (rank >= world && prefix) prefix[b] = acc;
+      total[b] = acc;
+    }
+  }
+}
+
 // ---- merger: AND-fold -----------------------------------------------------------------------
 // partial[g][:] = AND of states in group g (16 B per thread, 8 independent streaming loads in
 // flight; states are read once, so the loads bypass cache retention).
@@ -2615,6 +2642,16 @@ int kbz_triage_batch_device(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_
   if (kbz_shard_link(c, nullptr, nullptr, 1, nullptr, nullptr, stream)) return -1;
   if (kbz_shard_reduce(c, stream)) return -1;
   return kbz_shard_finish(c, nullptr, c->total, hnb_out, stream);
+}
+
+int kbz_or_prefix_total(uint8_t *prefix_out, uint8_t *total_out, const uint8_t *in, size_t rank,
+                        size_t world, size_t bytes, void *stream) {
+  if (!total_out || (!in && world)) return fail("null argument");
+  if (bytes == 0) return 0;
+  hipLaunchKernelGGL(k_or_prefix_total, dim3(cdiv(bytes, 16 * 256)), dim3(256), 0,
+                     (hipStream_t)stream, prefix_out, total_out, in, rank, world, bytes);
+  HIP_TRY(hipGetLastError());
+  return 0;
 }
 
 int kbz_or_reduce(uint8_t *out, const uint8_t *in, size_t r_lo, size_t r_hi, size_t bytes,

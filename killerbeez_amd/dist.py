@@ -12,7 +12,8 @@ the OR of the coverage seen by the ranks before it:
   3. local OR aggregate per virgin map (kbz_shard_reduce)
   4. all-gather of the aggregates (nclass * map_size bytes per rank) -> prefix = OR of earlier
      ranks, total = OR of all ranks.  RCCL has no bitwise reductions, so this is an
-     all-gather plus a local OR (kbz_or_reduce), ~8 x 64 KiB over xGMI: latency-bound.
+     all-gather plus one local OR pass for both (kbz_or_prefix_total), ~8 x 64 KiB over xGMI:
+     latency-bound.
   5. local resolve with the prefix; every rank applies V' = V & ~total, so the virgin maps
      stay identical on all ranks.
 
@@ -20,6 +21,8 @@ The engine is any object with the shard_* methods of killerbeez_amd.triage.Triag
 (tests plug a CPU engine in to exercise this protocol with the gloo backend).
 """
 from __future__ import annotations
+
+import time
 
 import torch
 import torch.distributed as dist
@@ -32,32 +35,63 @@ def split_counts(n_total: int, world: int) -> list[int]:
 
 
 def _all_gather(t: torch.Tensor, world: int, group=None) -> torch.Tensor:
-    parts = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(parts, t, group=group)
-    return torch.stack(parts)
+    """[world, *t.shape]: one all_gather_into_tensor into a flat buffer (no per-rank list, no
+    stack; gloo accepts only the flat output shape)."""
+    t = t.contiguous()
+    out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t.reshape(-1), group=group)
+    return out.view(world, *t.shape)
+
+
+class _Clock:
+    """Phase timing of one rank's sharded batch: HIP events on the current stream when the
+    tensors live on a GPU (read after the batch), wall clock otherwise."""
+
+    def __init__(self, device):
+        self.cuda = torch.device(device).type == "cuda"
+        self.marks = []
+
+    def mark(self, name):
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.marks.append((name, e))
+        else:
+            self.marks.append((name, time.perf_counter()))
+
+    def spans(self):
+        """{phase: ms} between consecutive marks (phase = the later mark's name)."""
+        out = {}
+        for (_, a), (name, b) in zip(self.marks, self.marks[1:]):
+            ms = a.elapsed_time(b) if self.cuda else 1e3 * (b - a)
+            out[name] = out.get(name, 0.0) + ms
+        return out
 
 
 def triage_sharded(engine, traces, outcome, counts, rank, world, want=1, group=None,
                    device=None, timings=None):
     """Run one rank's part of a sharded batch.  counts[r] = number of traces on rank r (host
-    ints, known to every rank).  Returns the engine's output dict (hnb, h32, ...)."""
+    ints, known to every rank).  Returns the engine's output dict (hnb, h32, ...).
+    timings: a list that receives this batch's phase times {pass1, link, reduce, collective,
+    finish} in ms (HIP events on a GPU, read with timing_summary after the steps)."""
     device = device if device is not None else traces.device
-    ev = None
-    if timings is not None:
-        ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
-        ev[0].record()
+    clk = _Clock(device) if timings is not None else None
+    mark = clk.mark if clk else (lambda name: None)
+    mark("start")
     out = engine.shard_begin(traces, outcome, want)
-    if ev is not None:
-        ev[1].record()
-        timings.append(ev)
+    mark("pass1")
     nonempty = [r for r in range(world) if counts[r] > 0]
     if engine.mode == MODE_DYNAMORIO:
         m = engine.map_size
-        buf = torch.zeros(m + 8, dtype=torch.uint8, device=device)  # [last row | hash pair]
+        # [last row | hash pair | pad]: map_size + 16 bytes, so every gathered row stays
+        # 16-byte aligned (k_chain reads rows with 16-byte loads)
+        buf = torch.zeros(m + 16, dtype=torch.uint8, device=device)
         engine.shard_last_row(buf[:m])
-        engine.shard_last_hash(buf[m:].view(torch.int32))
+        engine.shard_last_hash(buf[m:m + 8].view(torch.int32))
+        mark("link")
         bufs = _all_gather(buf, world, group) if world > 1 else buf.view(1, -1)
-        rows, pairs = bufs[:, :m], bufs[:, m:].view(torch.int32)
+        mark("collective")
+        rows, pairs = bufs[:, :m], bufs[:, m:m + 8].view(torch.int32)
         prev = [r for r in nonempty if r < rank]
         p = prev[-1] if prev else None
         g = nonempty[-1] if nonempty else None
@@ -66,21 +100,38 @@ def triage_sharded(engine, traces, outcome, counts, rank, world, want=1, group=N
                           None if g is None else rows[g])
     else:
         engine.shard_link(None, None, True, None, None)
+    mark("link")
     engine.shard_reduce()
     nb = engine.shard_aggregate_bytes()
     agg = torch.empty(nb, dtype=torch.uint8, device=device)
     engine.shard_aggregate(agg)
+    mark("reduce")
     if world > 1:
         allagg = _all_gather(agg, world, group)
+        mark("collective")
         total = torch.empty(nb, dtype=torch.uint8, device=device)
-        engine.or_reduce(total, allagg, 0, world, nb)
-        prefix = None
-        if rank > 0:
-            prefix = torch.empty(nb, dtype=torch.uint8, device=device)
-            engine.or_reduce(prefix, allagg, 0, rank, nb)
+        prefix = torch.empty(nb, dtype=torch.uint8, device=device) if rank > 0 else None
+        engine.or_prefix_total(prefix, total, allagg, rank, world, nb)
     else:
         total, prefix = agg, None
-    return engine.shard_finish(prefix, total)
+    res = engine.shard_finish(prefix, total)
+    mark("finish")
+    if clk is not None:
+        timings.append(clk)
+    return res
+
+
+def timing_summary(timings):
+    """Mean ms per batch of each phase over the recorded batches (waits for their events)."""
+    if not timings:
+        return {}
+    if timings[0].cuda:
+        torch.cuda.synchronize()
+    tot = {}
+    for clk in timings:
+        for k, v in clk.spans().items():
+            tot[k] = tot.get(k, 0.0) + v
+    return {k: v / len(timings) for k, v in tot.items()}
 
 
 # ---- merger across GPUs (BASELINE config 4; SURVEY.md §8(e)) ----------------------------------

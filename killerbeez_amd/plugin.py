@@ -51,9 +51,12 @@ def lib():
     global _PLUGIN
     if _PLUGIN is None:
         _lib.lib()  # the HIP library first (the plugin links it)
-        if not os.path.exists(_build.PLUGIN_LIB):
+        # KBZ_PLUGIN_LIB: an alternative build of the same sources (scripts/sanitize.sh loads
+        # its ASan + UBSan build this way)
+        path = os.environ.get("KBZ_PLUGIN_LIB") or _build.PLUGIN_LIB
+        if not os.path.exists(path):
             _build.build_plugin()
-        L = C.CDLL(_build.PLUGIN_LIB)
+        L = C.CDLL(path)
         for name in PLUGINS:
             for fn, (res, args) in _FN.items():
                 f = getattr(L, f"kbz_{name}_{fn}")

@@ -273,6 +273,15 @@ class TriageContext:
     def or_reduce(out, stacked, r_lo, r_hi, nbytes, stream=None):
         return or_reduce(out, stacked, r_lo, r_hi, nbytes, stream)
 
+    @staticmethod
+    def or_prefix_total(prefix, total, stacked, rank, world, nbytes, stream=None):
+        """prefix = OR of rows [0, rank) (None: skipped), total = OR of all rows, one launch."""
+        check(lib().kbz_or_prefix_total(None if prefix is None else C.c_void_p(prefix.data_ptr()),
+                                        C.c_void_p(total.data_ptr()),
+                                        C.c_void_p(stacked.data_ptr()), rank, world, nbytes,
+                                        _stream_handle(stream)), "kbz_or_prefix_total")
+        return prefix, total
+
 
 # ---- stateless device helpers ------------------------------------------------------------------
 

@@ -48,9 +48,10 @@ def _p(a):
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
+        path = os.environ.get("KBZ_ORACLE_LIB") or LIB_PATH  # scripts/sanitize.sh: ASan build
+        if not os.path.exists(path):
             build()
-        L = C.CDLL(LIB_PATH)
+        L = C.CDLL(path)
         L.kbzo_count_class.restype = C.c_uint8
         L.kbzo_count_class.argtypes = [C.c_uint8]
         L.kbzo_classify_counts.argtypes = [C.c_void_p, C.c_size_t]

@@ -17,7 +17,7 @@ import torch.multiprocessing as mp
 
 import oracle
 from killerbeez_amd import synth
-from killerbeez_amd.dist import split_counts, triage_sharded
+from killerbeez_amd.dist import split_counts, timing_summary, triage_sharded
 
 M = 4096
 
@@ -101,6 +101,23 @@ class CpuShardEngine:
         out.copy_(torch.from_numpy(np.bitwise_or.reduce(stacked[lo:hi].numpy(), axis=0))
                   if hi > lo else torch.zeros(nb, dtype=torch.uint8))
 
+    @staticmethod
+    def or_prefix_total(prefix, total, stacked, rank, world, nb):
+        """One pass over the gathered aggregates, as kbz_or_prefix_total does it."""
+        acc = np.zeros(nb, np.uint8)
+        rows = stacked.numpy()
+        for r in range(world):
+            if r == rank and prefix is not None:
+                prefix.copy_(torch.from_numpy(acc.copy()))
+            acc |= rows[r]
+        total.copy_(torch.from_numpy(acc))
+        # the fused pass equals the two separate reductions it replaces
+        two = [torch.empty(nb, dtype=torch.uint8) for _ in range(2)]
+        CpuShardEngine.or_reduce(two[0], stacked, 0, world, nb)
+        CpuShardEngine.or_reduce(two[1], stacked, 0, rank, nb)
+        assert torch.equal(two[0], total)
+        assert prefix is None or torch.equal(two[1], prefix)
+
     def shard_finish(self, prefix, total):
         pre = np.zeros((self.nc, M), np.uint8) if prefix is None else prefix.numpy().reshape(self.nc, M)
         tot = total.numpy().reshape(self.nc, M)
@@ -121,14 +138,16 @@ def _worker(rank, world, port, mode, counts, seed, q):
         t[51] = t[50]
     lo = sum(counts[:rank])
     eng = CpuShardEngine(mode, np.full((3, M), 0xFF, np.uint8))
-    hnbs = []
+    hnbs, timings = [], []
     for batch in range(2):  # two consecutive sharded batches: state carries over
         tt = t if batch == 0 else t[::-1].copy()
         oo = oc if batch == 0 else oc[::-1].copy()
         mine = torch.from_numpy(tt[lo:lo + counts[rank]].copy())
         out = triage_sharded(eng, mine, torch.from_numpy(oo[lo:lo + counts[rank]].copy()),
-                             counts, rank, world, device="cpu")
+                             counts, rank, world, device="cpu", timings=timings)
         hnbs.append(out["hnb"].numpy())
+    ph = timing_summary(timings)
+    assert {"pass1", "reduce", "collective", "finish"} <= set(ph), ph
     q.put((rank, hnbs, eng.V, eng.last))
     dist.destroy_process_group()
 

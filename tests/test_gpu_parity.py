@@ -323,14 +323,18 @@ def _run_shards(ctxs, shards, ocs, mode, device):
     nb = ctxs[0].shard_aggregate_bytes()
     allagg = torch.stack([c.shard_aggregate(torch.empty(nb, dtype=torch.uint8, device=device))
                           for c in ctxs])
-    total = torch.empty(nb, dtype=torch.uint8, device=device)
-    TriageContext.or_reduce(total, allagg, 0, world, nb)
     res = []
     for r, c in enumerate(ctxs):
-        prefix = None
+        # the fused prefix / total pass (kbz_or_prefix_total) against two kbz_or_reduce launches
+        total = torch.empty(nb, dtype=torch.uint8, device=device)
+        prefix = torch.empty(nb, dtype=torch.uint8, device=device) if r > 0 else None
+        TriageContext.or_prefix_total(prefix, total, allagg, r, world, nb)
+        t2 = torch.empty(nb, dtype=torch.uint8, device=device)
+        TriageContext.or_reduce(t2, allagg, 0, world, nb)
+        assert torch.equal(t2, total)
         if r > 0:
-            prefix = torch.empty(nb, dtype=torch.uint8, device=device)
-            TriageContext.or_reduce(prefix, allagg, 0, r, nb)
+            TriageContext.or_reduce(t2, allagg, 0, r, nb)
+            assert torch.equal(t2, prefix)
         res.append(c.shard_finish(prefix, total))
     torch.cuda.synchronize()
     for c in ctxs:
