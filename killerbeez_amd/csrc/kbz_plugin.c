@@ -187,6 +187,14 @@ static const char *js_skip(const char *p, int depth) {
   }
   return q;
 }
+/* the whole text is one well-formed JSON object (and nothing else but whitespace) */
+static int json_valid_object(const char *json) {
+  if (!json) return 0;
+  const char *p = js_ws(json);
+  if (*p != '{' || !(p = js_skip(p, 0))) return 0;
+  return *js_ws(p) == 0;
+}
+
 /* the value of top-level member `key` of the object `json`, or NULL (absent or malformed).  Keys
  * are compared as written (the formats here never escape key characters). */
 static const char *json_value(const char *json, const char *key) {
@@ -470,6 +478,10 @@ static kbz_plugin_t *plugin_dump_alloc(kbz_plugin_t *p) {
 
 static kbz_plugin_t *plugin_from_options(int mode, const char *options) {
   unsigned long long m = 65536, mb = 4096;
+  if (options && !json_valid_object(options)) {
+    set_err("options are not a well-formed JSON object");
+    return NULL;
+  }
   if (json_u64(options, "map_size", &m) < 0 || json_u64(options, "max_batch", &mb) < 0) {
     set_err("bad options (map_size / max_batch must be integers)");
     return NULL;
@@ -1041,6 +1053,10 @@ static int plugin_set_state(kbz_plugin_t *p, const char *json) {
     set_err("null argument");
     return 1;
   }
+  if (!json_valid_object(json)) {
+    set_err("state is not a well-formed JSON object");
+    return 1;
+  }
   unsigned long long m = 0, h = 0, lw = 0, ls = 0;
   const int hm = json_u64(json, "map_size", &m);
   if (hm < 0 || (hm == 1 && m != p->map_size)) {
@@ -1223,7 +1239,10 @@ static int decode_state_file(const files_job_t *j, const char *path, uint8_t *ro
   }
   unsigned long long ms = 0;
   int rc = 0;
-  if (json_u64(text, "map_size", &ms) == 1 && ms != m) {
+  if (!json_valid_object(text)) {
+    snprintf(err, errn, "%s: not a well-formed JSON object", path);
+    rc = -1;
+  } else if (json_u64(text, "map_size", &ms) == 1 && ms != m) {
     snprintf(err, errn, "%s: map_size %llu differs from the options' %zu", path, ms, m);
     rc = -1;
   } else if (c->per_module) {  /* dynamorio_set_state :1330-1349: modules matched by name */

@@ -17,7 +17,7 @@ from hypothesis import strategies as st
 from killerbeez_amd import plugin as P
 
 M = 256  # smallest map: 3 x 512 hex digits per afl state
-SETTINGS = settings(max_examples=150, deadline=None,
+SETTINGS = settings(max_examples=150, deadline=None, derandomize=True,
                     suppress_health_check=[HealthCheck.too_slow])
 
 json_leaf = st.one_of(st.none(), st.booleans(), st.integers(-2**70, 2**70),
