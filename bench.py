@@ -32,6 +32,8 @@ from __future__ import annotations
 
 import argparse
 import json
+
+import numpy as np
 import os
 import socket
 import subprocess
@@ -337,6 +339,51 @@ def crash_variant(args, pool, barrier_sync, dev, steps=5):
                     f"virgin_crash), own context, {'with' if want else 'no'} hash32"}
 
 
+def novelty_heavy(args, mode, want, batches, dev, steps=5):
+    """Campaign starts, new targets, freshly merged states: every step triages a never-seen batch
+    against all-0xff virgin maps (the maps are reset between steps, outside the timed region),
+    on a context of its own that already ran one batch (first-launch costs excluded).  Per step:
+    HIP events around the triage; per stage: the library's stage timing."""
+    import torch
+
+    from killerbeez_amd.triage import TriageContext
+
+    B, M = args.batch, args.map_size
+    fresh = np.full((3, M), 0xFF, np.uint8)
+    with TriageContext(M, mode, B) as c:
+        out = {"hnb": torch.empty(B, dtype=torch.uint8, device=dev)}
+        if want:
+            out["h32"] = torch.empty(B, dtype=torch.int32, device=dev)
+        c.triage(*batches[0], want, out=out)  # warm: first launches, allocations
+        c.sync()
+        ms, p1, claims = [], [], []
+        stages = {}
+        for i in range(steps):
+            c.set_virgin(fresh)
+            c.last_hash = 0
+            t, oc = batches[(i + 1) % len(batches)]
+            torch.cuda.synchronize()
+            c.time_pass1(True)
+            c.time_stages(True)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            c.triage(t, oc, want, out=out)
+            b.record()
+            b.synchronize()
+            ms.append(a.elapsed_time(b))
+            p1.append(c.time_pass1(False)[0])
+            st, _ = c.time_stages(False)
+            for k, v in st.items():
+                stages[k] = stages.get(k, 0.0) + v / steps
+            c.sync()
+            claims.append(c.stats()["claims"])
+    return {"ms_per_step": round(sum(ms) / steps, 4), "pass1_ms": round(sum(p1) / steps, 4),
+            "stage_ms": {k: round(v, 4) for k, v in stages.items()},
+            "claims_per_batch": int(sum(claims) / steps),
+            "what": f"{steps} never-seen batches, each on all-0xff virgin maps (reset between "
+                    "steps), own warmed-up context"}
+
+
 def main_triage(args):
     import torch
 
@@ -379,6 +426,7 @@ def main_triage(args):
         barrier_sync(world, dev)
         ctx.sync()
         ctx.time_pass1(True)
+        ctx.time_stages(True)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         t0 = time.perf_counter()
         ev[0].record()
@@ -388,10 +436,13 @@ def main_triage(args):
         barrier_sync(world, dev)
         el = time.perf_counter() - t0
         ms, launches = ctx.time_pass1(False)
+        st, nb = ctx.time_stages(False)
+        stage_log.append({k2: round(v / max(1, nb), 4) for k2, v in st.items()})
         ctx.sync()
         r = (max_over_ranks(el, world, dev), ms / max(1, launches))
         return r + (ev[0].elapsed_time(ev[1]),) if events else r
 
+    stage_log = []  # per timed() call: mean ms per batch of each stage after pass 1
     # warmup on fresh batches (the first one on all-0xff virgin maps, timed by itself)
     _, _, cold_ms = timed(pool[:1], 1, events=True)
     for i in range(1, args.warmup):
@@ -407,7 +458,8 @@ def main_triage(args):
     ms_per_step = 1e3 * elapsed / args.steps
     achieved = B * M / (pass1_ms * 1e-3) / 1e9  # GB/s, algorithmic bytes of one launch
     variants = {"cold_first_batch_ms": round(cold_ms, 4),
-                "last_fresh_batch_work": fresh_stats}
+                "last_fresh_batch_work": fresh_stats,
+                "stage_ms_per_step": stage_log[-1]}
     if not args.no_variants:
         seen = pool[-2:]
         el2, p2 = timed(seen, args.steps)
@@ -432,6 +484,7 @@ def main_triage(args):
                         "repeating their predecessor (last-hash skips), virgin carried"}
         if world == 1:
             variants["afl_all_crash_simplify"] = crash_variant(args, pool, barrier_sync, dev)
+            variants["novelty_heavy"] = novelty_heavy(args, mode, want, fresh, dev)
     del pool, fresh
     torch.cuda.empty_cache()  # the PMC child run below allocates its own batches
     traffic = None

@@ -111,6 +111,13 @@ int kbz_ctx_stats(kbz_ctx_t *ctx, uint32_t *out);
  * the previous call (waiting for them), then enables (enable != 0) or disables timing of later
  * launches.  Diagnostics only (bench.py's roofline). */
 int kbz_ctx_time_pass1(kbz_ctx_t *ctx, int enable, double *total_ms, uint32_t *launches);
+/* The same for the pipeline's other stages (k_skip, k_chain, k_total, k_scan, k_resolve,
+ * k_pack): stage_ms[KBZ_NSTAGES] gets each stage's summed duration over the batches timed since
+ * the previous call (index KBZ_STAGE_*; pass 1 stays with kbz_ctx_time_pass1, slot 0 is 0),
+ * *batches how many batches finished.  Diagnostics only (bench.py). */
+enum kbz_stage { KBZ_STAGE_PASS1 = 0, KBZ_STAGE_SKIP = 1, KBZ_STAGE_LINK = 2, KBZ_STAGE_REDUCE = 3,
+                 KBZ_STAGE_SCAN = 4, KBZ_STAGE_RESOLVE = 5, KBZ_STAGE_PACK = 6, KBZ_NSTAGES = 7 };
+int kbz_ctx_time_stages(kbz_ctx_t *ctx, int enable, double *stage_ms, uint32_t *batches);
 
 /* ---- batched triage ------------------------------------------------------------------------ */
 /* traces:   device, n rows of map_size raw 8-bit hit counters, row j at traces + j*stride

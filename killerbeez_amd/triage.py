@@ -76,6 +76,17 @@ class TriageContext:
               "kbz_ctx_time_pass1")
         return ms.value, k.value
 
+    STAGES = ("pass1", "skip", "link", "reduce", "scan", "resolve", "pack")
+
+    def time_stages(self, enable: bool = True):
+        """-> ({stage: summed ms}, batches) of the stages after pass 1 (k_skip ... k_pack) timed
+        since the last call; then times later batches iff `enable`."""
+        ms = np.zeros(len(self.STAGES), np.float64)
+        nb = C.c_uint32()
+        check(lib().kbz_ctx_time_stages(self._h, int(bool(enable)), _np_ptr(ms), C.byref(nb)),
+              "kbz_ctx_time_stages")
+        return {k: float(v) for k, v in zip(self.STAGES[1:], ms[1:])}, nb.value
+
     # -- lifetime --------------------------------------------------------------------------
     def close(self):
         if getattr(self, "_h", None):
