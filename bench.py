@@ -71,6 +71,8 @@ def parse():
     p.add_argument("--workload", default="config2",
                    choices=["config2", "config3", "merge", "stream", "plugin"])
     p.add_argument("--states", type=int, default=100000, help="merge workload: states (total)")
+    p.add_argument("--no-selfcheck", dest="selfcheck", action="store_false",
+                   help=argparse.SUPPRESS)  # PMC child runs: only the timed folds' kernels
     a = p.parse_args()
     if a.workload == "config3":
         if a.batch == 65536:
@@ -249,9 +251,9 @@ def cpu_baseline_all_cores(traces_dev, outcome_dev, mode, seconds):
 
 # ---- roofline traffic (PMC) --------------------------------------------------------------------
 
-def _pmc_pass(counter, workload_args, outdir, timeout=150):
+def _pmc_pass(counter, workload_args, outdir, timeout=150, kernel="k_pass1"):
     """One rocprofv3 --pmc pass over a short child run; per-dispatch values of `counter` for
-    the pass-1 kernel, in launch order."""
+    the kernels whose name contains `kernel` (default: pass 1), in launch order."""
     import csv
     import glob
 
@@ -263,7 +265,7 @@ def _pmc_pass(counter, workload_args, outdir, timeout=150):
     vals = []
     for f in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "k_pass1" in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
+            if kernel in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
                 vals.append((int(r.get("Dispatch_Id", 0) or 0), float(r["Counter_Value"])))
     return [v for _, v in sorted(vals)]
 
@@ -288,6 +290,27 @@ def live_traffic(args, warmup=1, steps=4):
             "source": f"live rocprofv3 --pmc, {len(fetch)} fresh-batch dispatches: "
                       f"FETCH_SIZE x2 = {2.0 * med(fetch) * 1024:.0f} B + WRITE_SIZE = "
                       f"{med(write) * 1024:.0f} B"}
+
+
+def merge_traffic(args, warmup=1, steps=3):
+    """HBM bytes of one local AND-fold of the merge leg (k_and_groups tree + k_and_rows), from
+    PMC like live_traffic: the fold kernels' per-dispatch FETCH_SIZE x2 + WRITE_SIZE summed over
+    the timed steps, divided by the steps (the first `warmup` steps' kernels are skipped)."""
+    import tempfile
+
+    wa = ["--workload", "merge", "--states", str(args.states), "--warmup", str(warmup),
+          "--steps", str(steps), "--seed", str(args.seed), "--no-selfcheck"]
+    with tempfile.TemporaryDirectory() as d:
+        fetch = _pmc_pass("FETCH_SIZE", wa, os.path.join(d, "f"), kernel="k_and_")
+        write = _pmc_pass("WRITE_SIZE", wa, os.path.join(d, "w"), kernel="k_and_")
+    per = len(fetch) // (warmup + steps)  # every step launches the same fold kernels
+    if not fetch or not write or per == 0:
+        return None
+    tot = 2.0 * sum(fetch[per * warmup:per * (warmup + steps)]) * 1024 + \
+        sum(write[per * warmup:per * (warmup + steps)]) * 1024
+    return {"bytes": tot / steps,
+            "source": f"live rocprofv3 --pmc: FETCH_SIZE x2 + WRITE_SIZE of the {per} fold "
+                      f"kernels of each of {steps} steps"}
 
 
 def stored_traffic(workload):
@@ -606,11 +629,12 @@ def main_merge(args):
     barrier_sync(world, dev)
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
     ms = sum(a.elapsed_time(b) for a, b in fold_ev) / len(fold_ev)
-    if world == 1:  # size-independent property: the fold equals the AND of the halves' folds
+    if world == 1 and args.selfcheck:  # size-independent: the fold = AND of the halves' folds
         halves = merge_and(states[: n // 2]) & merge_and(states[n // 2:])
         if not torch.equal(halves, out):
             raise SystemExit("merge self-check failed")
     bytes_ = n * sb
+    traffic = {"bytes": None, "source": "not measured (--no-pmc or N > 1)"}
     res = {"metric": "merger states AND-folded/sec (3 x 64 KiB virgin maps per state)",
            "value": round(n_all * args.steps / el, 1), "unit": "states/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup,
@@ -623,10 +647,20 @@ def main_merge(args):
            "roofline": {"bound": "hbm", "achieved": round(bytes_ / (ms * 1e-3) / 1e9, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(bytes_ / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                        "traffic": None, "kernel": "k_and_groups + k_and_rows (one local fold)",
+                        "traffic": traffic["bytes"], "traffic_source": traffic["source"],
+                        "kernel": "k_and_groups + k_and_rows (one local fold)",
                         "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": bytes_}}
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = merge_cpu_baseline(states, args.cpu_seconds)
+    if rank == 0 and world == 1 and args.pmc:
+        del states
+        torch.cuda.empty_cache()  # the PMC child run allocates its own states
+        try:
+            traffic = merge_traffic(args) or traffic
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal
+            traffic = {"bytes": None, "source": f"live PMC failed: {type(e).__name__}"}
+        res["roofline"]["traffic"] = traffic["bytes"]
+        res["roofline"]["traffic_source"] = traffic["source"]
     if rank == 0:
         print(json.dumps(res), flush=True)
     finish(world)

@@ -125,6 +125,15 @@ __device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[2]) {
   asm volatile("s_waitcnt vmcnt(%2)" : "+v"(r[0]), "+v"(r[1]) : "n"(N) : "memory");
 }
 template <int N>
+__device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[18]) {  // k_pass1d: + ignore words
+  asm volatile("s_waitcnt vmcnt(%18)"
+               : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
+                 "+v"(r[6]), "+v"(r[7]), "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]),
+                 "+v"(r[12]), "+v"(r[13]), "+v"(r[14]), "+v"(r[15]), "+v"(r[16]), "+v"(r[17])
+               : "n"(N)
+               : "memory");
+}
+template <int N>
 __device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[17]) {  // k_pass1n: 16 rows + virgin
   asm volatile("s_waitcnt vmcnt(%17)"
                : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
@@ -1148,7 +1157,10 @@ __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
   const uint32_t rlast = (uint32_t)((nrows - 1) * a.stride);
   // branch-free asm loads (see k_pass1s); tiles past t1 re-load tile t0
   auto load = [&](u32x4 (&r)[NR], uint32_t t) {
-    const uint32_t tt = t < t1 ? t : t0;
+    uint32_t tt = t < t1 ? t : t0;
+#ifdef KBZ_N_RR  // timing-only experiment: the same work, tiles dealt round-robin to the waves
+    tt = ((tt - t0) * NW + wave) % ntiles;
+#endif
 #pragma unroll
     for (int i = 0; i < NLD; i++) {
       const uint32_t off = min((uint32_t)(i * rstep + lr * a.stride), rlast);
@@ -1237,6 +1249,296 @@ __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
     }
   }
   drain_asm_loads(R);
+}
+
+// ---------------------------------------------------------------------------------------------
+// pass 1, DynamoRIO wide-map variant without lock-step (few chunks: BASELINE config 3, 16,384 x
+// 1 MiB = 256 chunks, one per CU).  has_new_coverage needs, per trace, the hash32 chain over the
+// classified words in order -- 131,072 dependent steps for a 1 MiB map, the floor of any batch --
+// and per column the OR over the chunk's rows.  The two halves only meet through an LDS ring of
+// RING tiles, NX + 2 waves per workgroup (dealt to the 4 SIMDs cyclically: wave w on SIMD w % 4):
+//   C     (wave 0) for t = 0, 1, ...: the 32 dependent hash32 steps of its row over tile t's k
+//         words, read (16 ds_read_b128, row per lane) one tile ahead so no LDS wait is ever on
+//         the chain; raised priority.  XXH64 (X64) from a ring of classified words.
+//   N     (wave 4, C's SIMD partner: light work, so the chain keeps its SIMD's issue) the
+//         neighbour test for the DynamoRIO skip: row r's words against row r-1's through DPP
+//         wave_shr:1 (the mix is a bijection: k equal <=> classified words equal; with ignore
+//         bytes the examined bytes are not the hashed ones, so X also writes classified &
+//         examined words to a second ring for N).
+//   X     (the other NX waves) each own every NX-th tile (t = x + NX q) and stream all 64 rows of
+//         it into a D-deep register ring (the k_pass1n layout: register i = row 4 i + l / 16,
+//         16-B slot l % 16), plus the tile's virgin (and ignore) words.  In registers:
+//         classify_counts, the column OR (lanes OR-reduced per slot), the still-virgin part
+//         stored like k_pass1s (chunk_or, segment atomics; tile flags OR'ed into LDS, written at
+//         the end), and the hash32 mix k = h32_mix(word & ignore) into ring slot t % RING
+//         (row-major, XOR-swizzled: conflict-free for row-per-lane reads); then ready[slot] = t.
+//         A slot is reused once C and N have read it (freed_c / freed_n).
+// No barrier inside the tile loop: the waves synchronise only through the LDS flags (polled with
+// s_sleep) and one barrier at the end (tile flags, neighbour flags).
+// ---------------------------------------------------------------------------------------------
+#ifndef KBZ_MAX_FW
+#define KBZ_MAX_FW 1024  // tile-flag words per class: maps up to 16 MiB
+#endif
+#ifndef KBZ_PASS1D_ABL  // timing-only ablations (wrong results): 1 = C skips the chain
+#define KBZ_PASS1D_ABL 0
+#endif
+template <bool IGN, bool X64, int NX, int RING, int D>
+__global__ __launch_bounds__(64 * (NX + 2), 1) void k_pass1d(Pass1Args a) {
+  static_assert(NX >= 3, "waves 1-3 are X waves, wave 4 is N");
+  constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = kChunk / RPI;
+  constexpr int NR = NLD + 1 + (IGN ? 1 : 0);  // rows, virgin words, ignore words
+  constexpr int TILE = kChunk * SLOTS;          // uint4 per ring slot
+  __shared__ uint4 kring[RING * TILE];
+  __shared__ uint4 wring[IGN ? RING * TILE : 1];
+  __shared__ uint4 tring[X64 ? RING * TILE : 1];
+  __shared__ int ready[RING], freed_c[RING], freed_n[RING];
+  __shared__ unsigned long long tfl_lds[KBZ_MAX_FW];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t chunk = blockIdx.x;
+  const uint64_t row0 = (uint64_t)chunk * kChunk;
+  const int nrows = (int)min((uint64_t)kChunk, (uint64_t)a.n - row0);
+  const uint32_t ntiles = a.map_size / TW;
+  for (int i = threadIdx.x; i < (int)a.nfw; i += blockDim.x) tfl_lds[i] = 0;
+  if (threadIdx.x < RING) {
+    ready[threadIdx.x] = -1;
+    freed_c[threadIdx.x] = freed_n[threadIdx.x] = (int)threadIdx.x - RING;  // slot s: tile s
+  }
+  __syncthreads();
+  volatile int *vready = ready, *vfc = freed_c, *vfn = freed_n;
+  const uint32_t seg = chunk / a.seg_len;
+  const int sw = lane & 15;
+  auto wait_ready = [&](uint32_t t) {
+    while (vready[t % RING] != (int)t) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+  };
+
+  if (wave == 0) {
+    // ------------------------------------------------------------ C: the chains
+    __builtin_amdgcn_s_setprio(3);
+    uint64_t h = (uint64_t)(kHashConst ^ a.map_size);
+    uint64_t x0 = kXP1 + kXP2, x1 = kXP2, x2 = 0, x3 = 0 - kXP1;
+    uint4 kb[2][SLOTS];  // tile t's k words in kb[t & 1], read one tile ahead
+    auto read_k = [&](uint32_t t, auto bc) {
+      constexpr int b = decltype(bc)::value;
+      const int sl = (int)(t % RING);
+#pragma unroll
+      for (int q = 0; q < SLOTS; q++) kb[b][q] = kring[sl * TILE + lane * SLOTS + (q ^ sw)];
+    };
+    auto chain = [&](uint32_t t, auto bc) {
+      constexpr int b = decltype(bc)::value;
+      if (!(KBZ_PASS1D_ABL & 1)) {
+#pragma unroll
+        for (int q = 0; q < SLOTS; q++) {
+          h = h32_step_fast(h, (uint64_t)kb[b][q].x | ((uint64_t)kb[b][q].y << 32));
+          h = h32_step_fast(h, (uint64_t)kb[b][q].z | ((uint64_t)kb[b][q].w << 32));
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < SLOTS; q++) h ^= kb[b][q].x;
+      }
+      if (X64) {
+        const int sl = (int)(t % RING);
+#pragma unroll 4
+        for (int q = 0; q < SLOTS; q++) {
+          const uint4 v = tring[sl * TILE + lane * SLOTS + (q ^ sw)];
+#pragma unroll
+          for (int e = 0; e < 2; e++) {
+            const uint64_t tw = ld_u64(v, e);
+            const int xl = (2 * q + e) & 3;
+            if (xl == 0) x0 = xx_round(x0, tw);
+            else if (xl == 1) x1 = xx_round(x1, tw);
+            else if (xl == 2) x2 = xx_round(x2, tw);
+            else x3 = xx_round(x3, tw);
+          }
+        }
+      }
+    };
+    // tile t: its words came in with the previous step; read t + 1's, chain t, then free t
+    // (XXH64 reads its own ring in the chain step, so the slot is freed after it)
+    KBZ_STAMP_DECL;
+    auto step = [&](uint32_t t, auto bc) {
+      constexpr int b = decltype(bc)::value;
+      // tile t + 1 already written: its reads overlap this chain; else they follow it
+      const bool more = t + 1 < ntiles;
+      const bool pre = more && vready[(t + 1) % RING] == (int)(t + 1);
+      asm volatile("" ::: "memory");
+      if (pre) read_k(t + 1, IntC<b ^ 1>{});
+      if (!X64 && lane == 0) vfc[t % RING] = (int)t;  // slot t's words are in registers
+      KBZ_STAMP(3);
+      chain(t, bc);
+      KBZ_STAMP(0);
+      if (more && !pre) {
+        wait_ready(t + 1);
+        KBZ_STAMP(1);
+        read_k(t + 1, IntC<b ^ 1>{});
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile t + 1's words have arrived
+      KBZ_STAMP(2);
+      if (X64 && lane == 0) vfc[t % RING] = (int)t;
+    };
+    if (ntiles) {
+      wait_ready(0);
+      read_k(0, IntC<0>{});
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    uint32_t t = 0;
+    for (; t + 1 < ntiles; t += 2) {
+      step(t, IntC<0>{});
+      step(t + 1, IntC<1>{});
+    }
+    if (t < ntiles) step(t, IntC<0>{});
+    KBZ_STAMP_FLUSH(chunk * 16 + wave);
+    if (lane < nrows) {
+      const uint32_t h32 = h32_final(h);
+      a.h32[row0 + lane] = h32;
+      if (X64 && a.x64) {
+        uint64_t xh = rotl64(x0, 1) + rotl64(x1, 7) + rotl64(x2, 12) + rotl64(x3, 18);
+        xh = xx_merge(xh, x0);
+        xh = xx_merge(xh, x1);
+        xh = xx_merge(xh, x2);
+        xh = xx_merge(xh, x3);
+        xh += a.map_size;
+        a.x64[row0 + lane] = xx_avalanche(xh);
+      }
+      if (row0 + lane == (uint64_t)a.n - 1) {
+        a.shard_last[0] = h32;
+        a.shard_last[1] = 1;
+      }
+    }
+    if (lane == 0) a.chunk_cls[chunk] = 1;  // DynamoRIO: one virgin map, every row in it
+  } else if (wave == 4) {
+    // ------------------------------------------------------------ N: the neighbour test
+    uint64_t nacc = 0;  // OR over the row's words of (word ^ previous row's word)
+    const uint4 *ring = IGN ? wring : kring;
+    for (uint32_t t = 0; t < ntiles; t++) {
+      wait_ready(t);
+      const int sl = (int)(t % RING);
+      uint4 vv[SLOTS];
+#pragma unroll
+      for (int q = 0; q < SLOTS; q++) vv[q] = ring[sl * TILE + lane * SLOTS + (q ^ sw)];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) vfn[sl] = (int)t;
+#pragma unroll
+      for (int q = 0; q < SLOTS; q++) {
+        const uint64_t w0 = (uint64_t)vv[q].x | ((uint64_t)vv[q].y << 32);
+        const uint64_t w1 = (uint64_t)vv[q].z | ((uint64_t)vv[q].w << 32);
+        nacc |= (w0 ^ from_prev_lane(w0)) | (w1 ^ from_prev_lane(w1));
+      }
+    }
+    // lane 0 has no predecessor in the wave: a placeholder (k_skip compares chunk starts)
+    if (lane < nrows) a.neq[row0 + lane] = nacc != 0;
+  } else {
+    // ------------------------------------------------------------ X waves
+    const int xi = wave < 4 ? wave - 1 : wave - 2;  // 0..NX-1
+    const int lr = lane / SLOTS, ls = lane % SLOTS;
+    const uint8_t *lbase = a.traces + row0 * a.stride + ls * 16;
+    const uint32_t rstep = (uint32_t)(RPI * a.stride);
+    const uint32_t rlast = (uint32_t)((nrows - 1) * a.stride);
+    const uint8_t *vbase = a.vcur + (size_t)ls * 16;
+    const uint8_t *gbase = IGN ? a.ignore + (size_t)ls * 16 : nullptr;
+    const uint32_t nmine = ntiles > (uint32_t)xi ? (ntiles - 1 - xi) / NX + 1 : 0;
+    const uint32_t nb = (nmine + D - 1) / D * D;
+    auto tile_of = [&](uint32_t q) { return (uint32_t)xi + q * NX; };
+    // branch-free asm loads (see k_pass1s); steps past the wave's last tile re-load its first
+    auto load = [&](u32x4 (&r)[NR], uint32_t q) {
+      const uint32_t t = q < nmine ? tile_of(q) : (uint32_t)xi;
+      const uint32_t tt = t < ntiles ? t : 0;
+#pragma unroll
+      for (int i = 0; i < NLD; i++) {
+        const uint32_t off = min((uint32_t)(i * rstep + lr * a.stride), rlast);
+        asm_load16(r[i], lbase + (size_t)tt * TW + off);
+      }
+      asm_load16_cached(r[NLD], vbase + (size_t)tt * TW);
+      if (IGN) asm_load16_cached(r[NLD + 1], gbase + (size_t)tt * TW);
+    };
+    u32x4 R[D][NR];
+#pragma unroll
+    for (int d = 0; d < D; d++) load(R[d], d);
+    KBZ_STAMP_DECL;
+    for (uint32_t q0 = 0; q0 < nb; q0 += D) {
+#pragma unroll
+      for (int u = 0; u < D; u++) {
+        const uint32_t q = q0 + u;
+        const uint32_t t = tile_of(q);
+        vmcnt_wait_ring<(D - 1) * NR>(R[u]);
+        KBZ_STAMP(0);
+        // classify_counts in place, the column OR (rows past the end of a partial chunk are
+        // copies of its last row: OR-ing them changes nothing)
+        u32x4 o = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < NLD; i++) {
+          const u32x4 x = R[u][i];
+          R[u][i] = u32x4{classify4(x.x), classify4(x.y), classify4(x.z), classify4(x.w)};
+          o |= R[u][i];
+        }
+        o = or_lanes(o);
+        u32x4 m = o & R[u][NLD];  // still-virgin bits only (like k_pass1s)
+        if (lane >= SLOTS) m = u32x4{0, 0, 0, 0};
+        u32x4 igw = {~0u, ~0u, ~0u, ~0u};
+        if (IGN) igw = R[u][NLD + 1];
+        asm volatile("" : "+v"(m), "+v"(igw));  // no value of the slot live across its reload
+        const bool mine = q < nmine;
+        const int sl = (int)(t % RING);
+        KBZ_STAMP(1);
+        if (mine)  // the slot is free once C and N have read tile t - RING from it
+          while (vfc[sl] != (int)t - RING || vfn[sl] != (int)t - RING)
+            __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+        KBZ_STAMP(2);
+#pragma unroll
+        for (int i = 0; i < NLD; i++) {
+          const int rr = RPI * i + lr;
+          const int idx = sl * TILE + rr * SLOTS + (ls ^ (rr & 15));
+          const u32x4 c = R[u][i];
+          const uint64_t c0 = (uint64_t)c.x | ((uint64_t)c.y << 32);
+          const uint64_t c1 = (uint64_t)c.z | ((uint64_t)c.w << 32);
+          const uint64_t g0 = (uint64_t)igw.x | ((uint64_t)igw.y << 32);
+          const uint64_t g1 = (uint64_t)igw.z | ((uint64_t)igw.w << 32);
+          const uint64_t k0 = h32_mix_mad(c0 & g0), k1 = h32_mix_mad(c1 & g1);
+          if (mine) {
+            kring[idx] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1,
+                                    (uint32_t)(k1 >> 32));
+            if (IGN) {  // the neighbour test looks at the bytes whose ignore byte is 0
+              const uint64_t e0 = c0 & ~nonzero_bytes8(g0), e1 = c1 & ~nonzero_bytes8(g1);
+              wring[idx] = make_uint4((uint32_t)e0, (uint32_t)(e0 >> 32), (uint32_t)e1,
+                                      (uint32_t)(e1 >> 32));
+            }
+            if (X64) tring[idx] = make_uint4(c.x, c.y, c.z, c.w);
+          }
+        }
+        if (mine) {
+          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the slot's words are written
+          asm volatile("" ::: "memory");
+          if (lane == 0) vready[sl] = (int)t;
+        }
+        load(R[u], q + D);  // the ring slot is free again
+        if (mine) {
+          const bool any = (m.x | m.y | m.z | m.w) != 0;
+          if (__ballot(any)) {
+            if (lane < SLOTS)
+              *(uint4 *)(a.chunk_or + (size_t)chunk * a.map_size + (size_t)t * TW + lane * 16) =
+                  make_uint4(m.x, m.y, m.z, m.w);
+            if (lane == 0) atomicOr(&tfl_lds[t >> 6], 1ull << (t & 63));
+          }
+          if (any) {
+            unsigned long long *sp = (unsigned long long *)(a.segor + (size_t)seg * a.map_size +
+                                                            (size_t)t * TW + lane * 16);
+            const uint64_t lo = (uint64_t)m.x | ((uint64_t)m.y << 32);
+            const uint64_t hi = (uint64_t)m.z | ((uint64_t)m.w << 32);
+            if (lo) atomicOr(sp, (unsigned long long)lo);
+            if (hi) atomicOr(sp + 1, (unsigned long long)hi);
+          }
+        }
+        KBZ_STAMP(3);
+      }
+    }
+    KBZ_STAMP_FLUSH(chunk * 16 + wave);
+    drain_asm_loads(R);
+  }
+  __syncthreads();  // every X wave's tile flags are in tfl_lds
+  uint64_t *tfbase = a.tflags + (size_t)chunk * a.nfw;
+  for (int i = threadIdx.x; i < (int)a.nfw; i += blockDim.x) tfbase[i] = tfl_lds[i];
 }
 
 // DynamoRIO last-hash skip: skip[j] = hash[j] == hash[j-1] (hash[-1] = previous exec's).
@@ -2053,6 +2355,15 @@ struct kbz_ctx {
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pass1;
   size_t ev_used_n = 0;
+  // kbz_ctx_time_stages: HIP events around the other stages' launches (stage id, start, end)
+  bool stage_timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_pool_used = 0;
+  struct StageRec {
+    int stage;
+    hipEvent_t a, b;
+  };
+  std::vector<StageRec> stage_recs;
 };
 
 namespace {
@@ -2116,6 +2427,7 @@ void free_ctx(kbz_ctx *c) {
     (void)hipEventDestroy(e.first);
     (void)hipEventDestroy(e.second);
   }
+  for (auto e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->work_stream) (void)hipStreamDestroy(c->work_stream);
@@ -2152,6 +2464,18 @@ void launch_abl(int depth, const Pass1Args &a, uint32_t chunks, hipStream_t s) {
   else hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, ABL, 4>), dim3(chunks), dim3(128), 0, s, a);
 }
 #endif
+#ifndef KBZ_PASS1D  // timing-only A/B builds: 0 = the lock-step k_pass1w for wide DynamoRIO batches
+#define KBZ_PASS1D 1
+#endif
+#ifndef KBZ_PASS1D_D
+#define KBZ_PASS1D_D 2
+#endif
+#ifndef KBZ_PASS1D_RING  // ring tiles of k_pass1d without ignore bytes / XXH64 (16 KiB each)
+#define KBZ_PASS1D_RING 4
+#endif
+#ifndef KBZ_PASS1D_NX  // X waves of k_pass1d: 6 = 8 waves, 2 per SIMD (C and N alone on SIMD 0);
+#define KBZ_PASS1D_NX 6  // 10 X waves with D = 1 (3 per SIMD): 3.72-3.77 vs 3.54 ms (r03_v7)
+#endif
 template <int MODE, bool IGN, bool X64>
 void launch_pass1(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s) {
 #ifdef KBZ_ABLATION
@@ -2164,7 +2488,11 @@ void launch_pass1(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s
   if (abl == 3) return launch_abl<MODE, IGN, X64, 3>(depth, a, chunks, s);
   return launch_abl<MODE, IGN, X64, 0>(depth, a, chunks, s);
 #else
-  if (pass1_is_wide(choice, chunks))
+  if (KBZ_PASS1D && MODE == KBZ_MODE_DYNAMORIO && pass1_is_wide(choice, chunks)) {
+    constexpr int RING = (IGN && X64) ? 2 : (IGN || X64) ? 3 : KBZ_PASS1D_RING;
+    hipLaunchKernelGGL((k_pass1d<IGN, X64, KBZ_PASS1D_NX, RING, KBZ_PASS1D_D>), dim3(chunks),
+                       dim3(64 * (KBZ_PASS1D_NX + 2)), 0, s, a);
+  } else if (pass1_is_wide(choice, chunks))
     hipLaunchKernelGGL((k_pass1w<MODE, IGN, X64, kWideNX, kWideNL, kWideD>), dim3(chunks),
                        dim3(64 * (kWideNL + kWideNX)), 0, s, a);
   else
@@ -2219,6 +2547,29 @@ int pass1_dispatch(kbz_ctx *c, const Pass1Args &a, uint32_t chunks, bool x64, bo
             : launch_pass1<KBZ_MODE_DYNAMORIO, false, false>(c->pass1, a, chunks, s);
   }
   HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+// Stage timing (kbz_ctx_time_stages): a start event now, the end event at stage_end.
+int stage_begin(kbz_ctx *c, hipStream_t s, hipEvent_t *out) {
+  *out = nullptr;
+  if (!c->stage_timing) return 0;
+  if (c->ev_pool_used + 2 > c->ev_pool.size()) {
+    for (int i = 0; i < 2; i++) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreateWithFlags(&e, KBZ_EVENT_SCOPE));
+      c->ev_pool.push_back(e);
+    }
+  }
+  *out = c->ev_pool[c->ev_pool_used++];
+  HIP_TRY(hipEventRecord(*out, s));
+  return 0;
+}
+int stage_end(kbz_ctx *c, hipStream_t s, int stage, hipEvent_t a) {
+  if (!a) return 0;
+  hipEvent_t b = c->ev_pool[c->ev_pool_used++];
+  HIP_TRY(hipEventRecord(b, s));
+  c->stage_recs.push_back({stage, a, b});
   return 0;
 }
 
@@ -2377,6 +2728,26 @@ int kbz_ctx_time_pass1(kbz_ctx_t *c, int enable, double *total_ms, uint32_t *lau
   c->timing = enable != 0;
   return 0;
 }
+int kbz_ctx_time_stages(kbz_ctx_t *c, int enable, double *stage_ms, uint32_t *batches) {
+  if (!c) return fail("null ctx");
+  DevGuard g(c->device);
+  double sum[KBZ_NSTAGES] = {0};
+  uint32_t nb = 0;
+  for (const auto &r : c->stage_recs) {
+    HIP_TRY(hipEventSynchronize(r.b));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
+    sum[r.stage] += ms;
+    nb += r.stage == KBZ_STAGE_PACK;
+  }
+  if (stage_ms)
+    for (int i = 0; i < KBZ_NSTAGES; i++) stage_ms[i] = sum[i];
+  if (batches) *batches = nb;
+  c->stage_recs.clear();
+  c->ev_pool_used = 0;
+  c->stage_timing = enable != 0;
+  return 0;
+}
 int kbz_ctx_set_pass1(kbz_ctx_t *c, int choice) {
   if (!c) return fail("null ctx");
   if (choice < KBZ_PASS1_AUTO || choice > KBZ_PASS1_WIDE) return fail("bad pass-1 choice");
@@ -2463,12 +2834,15 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
   if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, hashed, s)) return -1;
   if (ev) HIP_TRY(hipEventRecord(c->ev_pass1[c->ev_used_n - 1].second, s));
   if (c->mode == KBZ_MODE_DYNAMORIO) {  // the skip rule for rows j >= 1 needs no other shard
+    hipEvent_t st0;
+    if (stage_begin(c, s, &st0)) return -1;
     const unsigned row_blocks = cdiv(n, 256);
     hipLaunchKernelGGL(k_skip, dim3(row_blocks + c->cur_chunks - 1), dim3(256), 0, s, c->cur_h32,
                        c->neq, (uint32_t)n, c->skip, c->flags, c->fix_list, c->counters + 3,
                        c->bad_list, c->counters + 4, c->shard_last, traces, stride, c->ignore,
                        (uint32_t)c->M, row_blocks);
     HIP_TRY(hipGetLastError());
+    if (stage_end(c, s, KBZ_STAGE_SKIP, st0)) return -1;
   }
   c->stage = 1;
   return 0;
@@ -2540,8 +2914,11 @@ int kbz_shard_link(kbz_ctx_t *c, const uint32_t *prev_last, const uint8_t *prev_
     a.copy_dst = c->saved_row + (c->srow ^ 1) * M;
     a.saved_ok = c->counters + 6 + (c->srow ^ 1);
     const unsigned copy_blocks = a.copy_src ? std::min(64u, cdiv(M / 16, 256)) : 0;
+    hipEvent_t st0;
+    if (stage_begin(c, s, &st0)) return -1;
     hipLaunchKernelGGL(k_chain, dim3(1 + copy_blocks), dim3(256), 0, s, a);
     HIP_TRY(hipGetLastError());
+    if (stage_end(c, s, KBZ_STAGE_LINK, st0)) return -1;
     if (a.copy_src) {
       c->srow ^= 1;
       c->saved_valid = true;
@@ -2579,9 +2956,12 @@ int kbz_shard_reduce(kbz_ctx_t *c, void *stream) {
       fx.tflags = c->tflags;
       fx.nfw = c->nfw;
     }
+    hipEvent_t st0;
+    if (stage_begin(c, s, &st0)) return -1;
     hipLaunchKernelGGL(k_total, dim3(cdiv(c->M / 8, 256), 1, c->nc), dim3(256), 0, s, c->segor,
                        c->cur_nseg, c->nc, (uint32_t)c->M, c->segprev, c->total, fx);
     HIP_TRY(hipGetLastError());
+    if (stage_end(c, s, KBZ_STAGE_REDUCE, st0)) return -1;
   }
   c->stage = 3;
   return 0;
@@ -2607,24 +2987,31 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
   const int vn = c->vcur ^ 1;
   const uint8_t *ign = (c->mode == KBZ_MODE_DYNAMORIO) ? c->ignore : nullptr;
   const uint32_t nseg = c->cur_n ? c->cur_nseg : 1;
+  hipEvent_t st0;
+  if (stage_begin(c, s, &st0)) return -1;
   hipLaunchKernelGGL(k_scan, dim3(gx, nseg, c->nc), dim3(256), 0, s, c->chunk_or, c->chunk_cls,
                      c->cur_chunks, c->cur_seg_len, c->nc, (uint32_t)c->M, c->segprev, nseg,
                      c->total, prefix, total, c->V[c->vcur], c->V[vn], ign, c->items,
                      c->item_cap, c->counters, c->tflags, c->nfw,
                      c->mode == KBZ_MODE_DYNAMORIO ? c->flags : nullptr);
   HIP_TRY(hipGetLastError());
+  if (stage_end(c, s, KBZ_STAGE_SCAN, st0)) return -1;
   if (c->cur_n) {
+    if (stage_begin(c, s, &st0)) return -1;
     hipLaunchKernelGGL(k_resolve, dim3(512), dim3(256), 0, s, c->cur_traces, c->cur_stride,
                        (uint32_t)c->cur_n, c->mode, c->cur_outcome,
                        c->mode == KBZ_MODE_DYNAMORIO ? c->skip : nullptr, c->items, c->counters,
                        c->item_cap, c->hnb32, c->counters + 2);
     HIP_TRY(hipGetLastError());
+    if (stage_end(c, s, KBZ_STAGE_RESOLVE, st0)) return -1;
+    if (stage_begin(c, s, &st0)) return -1;
     hipLaunchKernelGGL(k_pack, dim3(cdiv(c->cur_n, 256)), dim3(256), 0, s, c->hnb32, c->cur_h32,
                        (uint32_t)c->cur_n, hnb_out ? hnb_out : (uint8_t *)nullptr,
                        (c->cur_h32_out && c->cur_h32_out != c->cur_h32) ? c->cur_h32_out : nullptr,
                        c->counters, c->mode == KBZ_MODE_DYNAMORIO ? c->flags : nullptr,
                        c->cur_chunks, c->shard_last, c->d_err);
     HIP_TRY(hipGetLastError());
+    if (stage_end(c, s, KBZ_STAGE_PACK, st0)) return -1;
   } else {
     // empty shard: k_skip may still have written the fix count / shard pair; re-arm them
     HIP_TRY(hipMemsetAsync(c->counters + 3, 0, 3 * sizeof(uint32_t), s));

@@ -1,9 +1,9 @@
 """Static check of pass 1's hand-counted VMEM waits (tools/vmem_hazard_cfg.py).
 
-The pass-1 kernels (k_pass1s, the wide-map k_pass1w and the no-hash k_pass1n) issue their prefetch loads from
+The pass-1 kernels (k_pass1s, the wide-map k_pass1w / k_pass1d and the no-hash k_pass1n) issue their prefetch loads from
 inline asm, which the compiler does not track: it may copy, reuse or overwrite a destination
 register before the hand-written `s_waitcnt vmcnt(N)`.  This compiles the device code to ISA,
-walks every k_pass1s, k_pass1w and k_pass1n instantiation as a control-flow graph with an in-order vmcnt
+walks every k_pass1s, k_pass1w, k_pass1d and k_pass1n instantiation as a control-flow graph with an in-order vmcnt
 queue, and requires that no instruction touches a register whose load may still be in flight.
 """
 import os
@@ -27,11 +27,13 @@ def test_pass1_has_no_inflight_register_hazards(tmp_path, flags):
                            *flags, build.HIP_SOURCES[0], "-o", str(out)],
                           stderr=subprocess.DEVNULL)
     funcs = V.split_functions(out.read_text().split("\n"))
-    pass1 = {k: v for k, v in funcs.items() if any(p in k for p in ("k_pass1s", "k_pass1w", "k_pass1n"))}
+    pass1 = {k: v for k, v in funcs.items()
+             if any(p in k for p in ("k_pass1s", "k_pass1w", "k_pass1n", "k_pass1d"))}
     assert any("k_pass1s" in k for k in pass1), "no k_pass1s instantiation found in the ISA"
     if not flags:  # the ablation build compiles only k_pass1s
         assert sum("k_pass1w" in k for k in pass1) == 8, sorted(pass1)
         assert sum("k_pass1n" in k for k in pass1) == 4, sorted(pass1)
+        assert sum("k_pass1d" in k for k in pass1) == 4, sorted(pass1)
     bad = {k: V.scan_function(v) for k, v in pass1.items()}
     bad = {k: v[:3] for k, v in bad.items() if v}
     assert not bad, bad

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Diagnostic: run k_pass1w on BASELINE config 3 (16,384 dense x 1 MiB) with a -DKBZ_STAMPS
-build (KBZ_HIP_LIB=...) and print, per wave of the workgroup, the median cycles per launch in
-{work, barrier wait, vmcnt wait / finish, LDS fill}.  Not part of the product."""
+"""Diagnostic: run the wide DynamoRIO pass 1 on BASELINE config 3 (16,384 dense x 1 MiB) with a
+-DKBZ_STAMPS build (KBZ_HIP_LIB=...) and print, per wave of the workgroup, the median cycles per
+launch in its four stamp phases.  k_pass1w: {work, barrier wait, vmcnt wait / finish, LDS fill};
+k_pass1d (KBZ_STAMP_NAMES=d): C wave 0 {chain, ready wait, LDS read wait, flags}, X waves
+{vmcnt wait, classify+OR+mix, freed wait, ring writes+stores+loads}.  Not part of the product."""
 import ctypes as C
 import os
 import sys
@@ -26,7 +28,8 @@ torch.cuda.synchronize()
 buf = np.zeros(4096 * 2 * 4, np.uint64)
 f(buf.ctypes.data_as(C.c_void_p), buf.size)
 st = buf.reshape(-1, 16, 4)[:256].astype(np.float64)  # [chunk][wave][phase]
-names = ["work|xform", "barrier", "vmcnt|reads", "fill|finish"]
+names = (["p0", "p1", "p2", "p3"] if os.environ.get("KBZ_STAMP_NAMES") == "d"
+         else ["work|xform", "barrier", "vmcnt|reads", "fill|finish"])
 for w in range(16):
     tot = st[:, w, :].sum(axis=1)
     if np.median(tot) == 0:
