@@ -445,11 +445,11 @@ def main_triage(args):
 
     def timed(batches, k, events=False):
         """k steps over batches[i % len], bracketed by barrier + synchronize; max over ranks.
-        Returns (seconds, pass-1 ms per launch[, device ms of the k steps])."""
+        Returns (seconds, pass-1 ms per launch[, device ms of the k steps]).  Stage timing (two
+        events per stage) stays off here: it adds ~50 us per step; the warmup steps time stages."""
         barrier_sync(world, dev)
         ctx.sync()
         ctx.time_pass1(True)
-        ctx.time_stages(True)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         t0 = time.perf_counter()
         ev[0].record()
@@ -459,17 +459,18 @@ def main_triage(args):
         barrier_sync(world, dev)
         el = time.perf_counter() - t0
         ms, launches = ctx.time_pass1(False)
-        st, nb = ctx.time_stages(False)
-        stage_log.append({k2: round(v / max(1, nb), 4) for k2, v in st.items()})
         ctx.sync()
         r = (max_over_ranks(el, world, dev), ms / max(1, launches))
         return r + (ev[0].elapsed_time(ev[1]),) if events else r
 
-    stage_log = []  # per timed() call: mean ms per batch of each stage after pass 1
-    # warmup on fresh batches (the first one on all-0xff virgin maps, timed by itself)
+    # warmup on fresh batches (the first one on all-0xff virgin maps, timed by itself); the
+    # other warmup batches are fresh too and time the stages after pass 1
     _, _, cold_ms = timed(pool[:1], 1, events=True)
+    ctx.time_stages(True)
     for i in range(1, args.warmup):
         step(*pool[i % npool])
+    st, nb = ctx.time_stages(False)
+    stage_ms = {k2: round(v / max(1, nb), 4) for k2, v in st.items()}
     fresh = pool[args.warmup:] if npool > args.warmup else pool
     phase_log = [] if world > 1 else None
     elapsed, pass1_ms = timed(fresh, args.steps)
@@ -482,7 +483,8 @@ def main_triage(args):
     achieved = B * M / (pass1_ms * 1e-3) / 1e9  # GB/s, algorithmic bytes of one launch
     variants = {"cold_first_batch_ms": round(cold_ms, 4),
                 "last_fresh_batch_work": fresh_stats,
-                "stage_ms_per_step": stage_log[-1]}
+                "stage_ms_per_step": stage_ms,
+                "stage_ms_note": "fresh warmup batches 2..W, stage events on (off in the timed steps)"}
     if not args.no_variants:
         seen = pool[-2:]
         el2, p2 = timed(seen, args.steps)

@@ -1279,12 +1279,22 @@ __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
 #ifndef KBZ_MAX_FW
 #define KBZ_MAX_FW 1024  // tile-flag words per class: maps up to 16 MiB
 #endif
-#ifndef KBZ_PASS1D_ABL  // timing-only ablations (wrong results): 1 = C skips the chain
+#ifndef KBZ_PASS1D_ABL  // timing-only ablations (wrong results), bits: 1 = C skips the chain,
+                        // 2 = N only hands slots back, 4 = X skips classify, 8 = X skips the mix
 #define KBZ_PASS1D_ABL 0
 #endif
+#ifndef KBZ_PASS1D_SPEC  // 1: C reads tile t + 1's words inside chain(t) (see step)
+#define KBZ_PASS1D_SPEC 1
+#endif
+#ifndef KBZ_PASS1D_CN  // 1: without ignore bytes C runs the neighbour test itself, in its chain's
+#define KBZ_PASS1D_CN 0   // dependency bubbles (wave 4 idles with NX = 6, is an X wave with NX = 7)
+#endif
 template <bool IGN, bool X64, int NX, int RING, int D>
-__global__ __launch_bounds__(64 * (NX + 2), 1) void k_pass1d(Pass1Args a) {
-  static_assert(NX >= 3, "waves 1-3 are X waves, wave 4 is N");
+__global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
+  // X waves are the waves off SIMD 0 (3 of every 4): wave 0 is C, wave 4 is N, wave 8 idles
+  static_assert(NX == 6 || NX == 9, "6 or 9 X waves: 8 or 12 waves per workgroup");
+  // CN: C tests neighbours on its k words (wave 4 then idles)
+  constexpr bool CN = KBZ_PASS1D_CN && !IGN;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = kChunk / RPI;
   constexpr int NR = NLD + 1 + (IGN ? 1 : 0);  // rows, virgin words, ignore words
   constexpr int TILE = kChunk * SLOTS;          // uint4 per ring slot
@@ -1305,11 +1315,15 @@ __global__ __launch_bounds__(64 * (NX + 2), 1) void k_pass1d(Pass1Args a) {
     freed_c[threadIdx.x] = freed_n[threadIdx.x] = (int)threadIdx.x - RING;  // slot s: tile s
   }
   __syncthreads();
-  volatile int *vready = ready, *vfc = freed_c, *vfn = freed_n;
+  // the ring flags: relaxed workgroup-scope atomics on the LDS arrays themselves, so they are
+  // ds_read/ds_write (a volatile generic pointer compiles to flat accesses, and each of those
+  // waits vmcnt(0): every X wave's register-ring loads in flight)
+#define KBZ_FLD(arr, i) __hip_atomic_load(&(arr)[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+#define KBZ_FST(arr, i, v) __hip_atomic_store(&(arr)[i], (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
   const uint32_t seg = chunk / a.seg_len;
   const int sw = lane & 15;
   auto wait_ready = [&](uint32_t t) {
-    while (vready[t % RING] != (int)t) __builtin_amdgcn_s_sleep(1);
+    while (KBZ_FLD(ready, t % RING) != (int)t) __builtin_amdgcn_s_sleep(1);
     asm volatile("" ::: "memory");
   };
 
@@ -1325,13 +1339,29 @@ __global__ __launch_bounds__(64 * (NX + 2), 1) void k_pass1d(Pass1Args a) {
 #pragma unroll
       for (int q = 0; q < SLOTS; q++) kb[b][q] = kring[sl * TILE + lane * SLOTS + (q ^ sw)];
     };
+    uint32_t nacc_lo = 0, nacc_hi = 0;  // CN: OR over the row's words of (word ^ previous row's)
+    // SPEC: chain(t) also reads tile t + 1's words, one ds_read_b128 per two steps (they issue
+    // in the chain's dependency gaps instead of as a burst of 16 between two tiles)
     auto chain = [&](uint32_t t, auto bc) {
       constexpr int b = decltype(bc)::value;
+      const int sl1 = (int)((t + 1) % RING);
       if (!(KBZ_PASS1D_ABL & 1)) {
 #pragma unroll
         for (int q = 0; q < SLOTS; q++) {
-          h = h32_step_fast(h, (uint64_t)kb[b][q].x | ((uint64_t)kb[b][q].y << 32));
-          h = h32_step_fast(h, (uint64_t)kb[b][q].z | ((uint64_t)kb[b][q].w << 32));
+          if (KBZ_PASS1D_SPEC) {
+            kb[b ^ 1][q] = kring[sl1 * TILE + lane * SLOTS + (q ^ sw)];
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          const uint4 kq = kb[b][q];
+          h = h32_step_fast(h, (uint64_t)kq.x | ((uint64_t)kq.y << 32));
+          h = h32_step_fast(h, (uint64_t)kq.z | ((uint64_t)kq.w << 32));
+          if (CN) {  // 32-bit halves: wave_shr:1 with bound_ctrl (lane 0 reads 0)
+            nacc_lo |= (kq.x ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)kq.x, 0x138, 0xf, 0xf, true)) |
+                       (kq.z ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)kq.z, 0x138, 0xf, 0xf, true));
+            nacc_hi |= (kq.y ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)kq.y, 0x138, 0xf, 0xf, true)) |
+                       (kq.w ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)kq.w, 0x138, 0xf, 0xf, true));
+            asm volatile("" : "+v"(nacc_lo), "+v"(nacc_hi));  // ORed now, not deferred (spills)
+          }
         }
       } else {
 #pragma unroll
@@ -1357,14 +1387,40 @@ __global__ __launch_bounds__(64 * (NX + 2), 1) void k_pass1d(Pass1Args a) {
     // tile t: its words came in with the previous step; read t + 1's, chain t, then free t
     // (XXH64 reads its own ring in the chain step, so the slot is freed after it)
     KBZ_STAMP_DECL;
+#if KBZ_PASS1D_SPEC
+    // The flag of tile t + 1's slot is read before the chain's speculative reads of its words:
+    // a wave's LDS operations execute in order, so if the flag says "ready", the words are tile
+    // t + 1's.  Otherwise they are read again once it does.  Slot t + 1 is freed (without XXH64)
+    // when its words are in registers: at the end of step t.
+    auto step = [&](uint32_t t, auto bc) {
+      constexpr int b = decltype(bc)::value;
+      const bool more = t + 1 < ntiles;
+      const int f = KBZ_FLD(ready, (t + 1) % RING);
+      asm volatile("" ::: "memory");  // the flag read stays ahead of the word reads
+      KBZ_STAMP(3);
+      chain(t, bc);
+      KBZ_STAMP(0);
+      if (more && f != (int)(t + 1)) {
+        wait_ready(t + 1);
+        KBZ_STAMP(1);
+        read_k(t + 1, IntC<b ^ 1>{});
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile t + 1's words have arrived
+      KBZ_STAMP(2);
+      if (lane == 0) {
+        if (X64) KBZ_FST(freed_c, t % RING, (int)t);
+        else if (more) KBZ_FST(freed_c, (t + 1) % RING, (int)(t + 1));
+      }
+    };
+#else
     auto step = [&](uint32_t t, auto bc) {
       constexpr int b = decltype(bc)::value;
       // tile t + 1 already written: its reads overlap this chain; else they follow it
       const bool more = t + 1 < ntiles;
-      const bool pre = more && vready[(t + 1) % RING] == (int)(t + 1);
+      const bool pre = more && KBZ_FLD(ready, (t + 1) % RING) == (int)(t + 1);
       asm volatile("" ::: "memory");
       if (pre) read_k(t + 1, IntC<b ^ 1>{});
-      if (!X64 && lane == 0) vfc[t % RING] = (int)t;  // slot t's words are in registers
+      if (!X64 && lane == 0) KBZ_FST(freed_c, t % RING, (int)t);  // slot t's words are in registers
       KBZ_STAMP(3);
       chain(t, bc);
       KBZ_STAMP(0);
@@ -1375,12 +1431,14 @@ __global__ __launch_bounds__(64 * (NX + 2), 1) void k_pass1d(Pass1Args a) {
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile t + 1's words have arrived
       KBZ_STAMP(2);
-      if (X64 && lane == 0) vfc[t % RING] = (int)t;
+      if (X64 && lane == 0) KBZ_FST(freed_c, t % RING, (int)t);
     };
+#endif
     if (ntiles) {
       wait_ready(0);
       read_k(0, IntC<0>{});
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (KBZ_PASS1D_SPEC && !X64 && lane == 0) KBZ_FST(freed_c, 0, 0);
     }
     uint32_t t = 0;
     for (; t + 1 < ntiles; t += 2) {
@@ -1406,19 +1464,24 @@ __global__ __launch_bounds__(64 * (NX + 2), 1) void k_pass1d(Pass1Args a) {
         a.shard_last[1] = 1;
       }
     }
+    if (CN && lane < nrows) a.neq[row0 + lane] = (nacc_lo | nacc_hi) != 0;  // lane 0: placeholder, as N's
     if (lane == 0) a.chunk_cls[chunk] = 1;  // DynamoRIO: one virgin map, every row in it
-  } else if (wave == 4) {
+  } else if (wave == 4 && !CN) {
     // ------------------------------------------------------------ N: the neighbour test
     uint64_t nacc = 0;  // OR over the row's words of (word ^ previous row's word)
     const uint4 *ring = IGN ? wring : kring;
     for (uint32_t t = 0; t < ntiles; t++) {
       wait_ready(t);
       const int sl = (int)(t % RING);
+      if (KBZ_PASS1D_ABL & 2) {
+        if (lane == 0) KBZ_FST(freed_n, sl, (int)t);
+        continue;
+      }
       uint4 vv[SLOTS];
 #pragma unroll
       for (int q = 0; q < SLOTS; q++) vv[q] = ring[sl * TILE + lane * SLOTS + (q ^ sw)];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane == 0) vfn[sl] = (int)t;
+      if (lane == 0) KBZ_FST(freed_n, sl, (int)t);
 #pragma unroll
       for (int q = 0; q < SLOTS; q++) {
         const uint64_t w0 = (uint64_t)vv[q].x | ((uint64_t)vv[q].y << 32);
@@ -1428,9 +1491,11 @@ __global__ __launch_bounds__(64 * (NX + 2), 1) void k_pass1d(Pass1Args a) {
     }
     // lane 0 has no predecessor in the wave: a placeholder (k_skip compares chunk starts)
     if (lane < nrows) a.neq[row0 + lane] = nacc != 0;
+  } else if ((wave & 3) == 0) {
+    // idle (wave 8; wave 4 with CN): SIMD 0 is left to the chain
   } else {
     // ------------------------------------------------------------ X waves
-    const int xi = wave < 4 ? wave - 1 : wave - 2;  // 0..NX-1
+    const int xi = wave - 1 - wave / 4;  // 0..NX-1
     const int lr = lane / SLOTS, ls = lane % SLOTS;
     const uint8_t *lbase = a.traces + row0 * a.stride + ls * 16;
     const uint32_t rstep = (uint32_t)(RPI * a.stride);
@@ -1469,7 +1534,8 @@ __global__ __launch_bounds__(64 * (NX + 2), 1) void k_pass1d(Pass1Args a) {
 #pragma unroll
         for (int i = 0; i < NLD; i++) {
           const u32x4 x = R[u][i];
-          R[u][i] = u32x4{classify4(x.x), classify4(x.y), classify4(x.z), classify4(x.w)};
+          if (!(KBZ_PASS1D_ABL & 4))
+            R[u][i] = u32x4{classify4(x.x), classify4(x.y), classify4(x.z), classify4(x.w)};
           o |= R[u][i];
         }
         o = or_lanes(o);
@@ -1482,7 +1548,7 @@ __global__ __launch_bounds__(64 * (NX + 2), 1) void k_pass1d(Pass1Args a) {
         const int sl = (int)(t % RING);
         KBZ_STAMP(1);
         if (mine)  // the slot is free once C and N have read tile t - RING from it
-          while (vfc[sl] != (int)t - RING || vfn[sl] != (int)t - RING)
+          while (KBZ_FLD(freed_c, sl) != (int)t - RING || (!CN && KBZ_FLD(freed_n, sl) != (int)t - RING))
             __builtin_amdgcn_s_sleep(1);
         asm volatile("" ::: "memory");
         KBZ_STAMP(2);
@@ -1495,7 +1561,8 @@ __global__ __launch_bounds__(64 * (NX + 2), 1) void k_pass1d(Pass1Args a) {
           const uint64_t c1 = (uint64_t)c.z | ((uint64_t)c.w << 32);
           const uint64_t g0 = (uint64_t)igw.x | ((uint64_t)igw.y << 32);
           const uint64_t g1 = (uint64_t)igw.z | ((uint64_t)igw.w << 32);
-          const uint64_t k0 = h32_mix_mad(c0 & g0), k1 = h32_mix_mad(c1 & g1);
+          const uint64_t k0 = (KBZ_PASS1D_ABL & 8) ? c0 & g0 : h32_mix_mad(c0 & g0);
+          const uint64_t k1 = (KBZ_PASS1D_ABL & 8) ? c1 & g1 : h32_mix_mad(c1 & g1);
           if (mine) {
             kring[idx] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1,
                                     (uint32_t)(k1 >> 32));
@@ -1510,7 +1577,7 @@ __global__ __launch_bounds__(64 * (NX + 2), 1) void k_pass1d(Pass1Args a) {
         if (mine) {
           __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the slot's words are written
           asm volatile("" ::: "memory");
-          if (lane == 0) vready[sl] = (int)t;
+          if (lane == 0) KBZ_FST(ready, sl, (int)t);
         }
         load(R[u], q + D);  // the ring slot is free again
         if (mine) {
@@ -1540,6 +1607,8 @@ __global__ __launch_bounds__(64 * (NX + 2), 1) void k_pass1d(Pass1Args a) {
   uint64_t *tfbase = a.tflags + (size_t)chunk * a.nfw;
   for (int i = threadIdx.x; i < (int)a.nfw; i += blockDim.x) tfbase[i] = tfl_lds[i];
 }
+#undef KBZ_FLD
+#undef KBZ_FST
 
 // DynamoRIO last-hash skip: skip[j] = hash[j] == hash[j-1] (hash[-1] = previous exec's).
 // A skipped trace must not touch the virgin map.  Pass 1 OR'ed it into its chunk, which is
@@ -2490,8 +2559,9 @@ void launch_pass1(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s
 #else
   if (KBZ_PASS1D && MODE == KBZ_MODE_DYNAMORIO && pass1_is_wide(choice, chunks)) {
     constexpr int RING = (IGN && X64) ? 2 : (IGN || X64) ? 3 : KBZ_PASS1D_RING;
+    constexpr int NW = KBZ_PASS1D_NX / 3 * 4;
     hipLaunchKernelGGL((k_pass1d<IGN, X64, KBZ_PASS1D_NX, RING, KBZ_PASS1D_D>), dim3(chunks),
-                       dim3(64 * (KBZ_PASS1D_NX + 2)), 0, s, a);
+                       dim3(64 * NW), 0, s, a);
   } else if (pass1_is_wide(choice, chunks))
     hipLaunchKernelGGL((k_pass1w<MODE, IGN, X64, kWideNX, kWideNL, kWideD>), dim3(chunks),
                        dim3(64 * (kWideNL + kWideNX)), 0, s, a);
@@ -3067,8 +3137,8 @@ int kbz_sync(kbz_ctx_t *c, void *stream) {
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   uint32_t cnt[4];
   HIP_TRY(hipMemcpy(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost));
-#if defined(KBZ_XP_NOMIX) || defined(KBZ_XP_NOCLS)
-  cnt[2] = 0;  // timing-only builds with inconsistent results
+#if defined(KBZ_XP_NOMIX) || defined(KBZ_XP_NOCLS) || KBZ_PASS1D_ABL
+  cnt[1] = cnt[2] = 0;  // timing-only builds with inconsistent results
 #endif
   if (cnt[1] || cnt[2]) {  // sticky until reported here
     HIP_TRY(hipMemset(c->counters + 1, 0, 2 * sizeof(uint32_t)));
