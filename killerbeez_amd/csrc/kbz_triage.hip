@@ -1468,6 +1468,9 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
     if (lane == 0) a.chunk_cls[chunk] = 1;  // DynamoRIO: one virgin map, every row in it
   } else if (wave == 4 && !CN) {
     // ------------------------------------------------------------ N: the neighbour test
+#ifdef KBZ_PASS1D_NPRIO  // timing-only A/B
+    __builtin_amdgcn_s_setprio(KBZ_PASS1D_NPRIO);
+#endif
     uint64_t nacc = 0;  // OR over the row's words of (word ^ previous row's word)
     const uint4 *ring = IGN ? wring : kring;
     for (uint32_t t = 0; t < ntiles; t++) {
@@ -1496,6 +1499,9 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
   } else {
     // ------------------------------------------------------------ X waves
     const int xi = wave - 1 - wave / 4;  // 0..NX-1
+#ifdef KBZ_PASS1D_XPRIO  // timing-only A/B: the younger X waves of each SIMD at raised priority
+    if (wave >= 4) __builtin_amdgcn_s_setprio(KBZ_PASS1D_XPRIO);
+#endif
     const int lr = lane / SLOTS, ls = lane % SLOTS;
     const uint8_t *lbase = a.traces + row0 * a.stride + ls * 16;
     const uint32_t rstep = (uint32_t)(RPI * a.stride);
@@ -1543,7 +1549,10 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
         if (lane >= SLOTS) m = u32x4{0, 0, 0, 0};
         u32x4 igw = {~0u, ~0u, ~0u, ~0u};
         if (IGN) igw = R[u][NLD + 1];
-        asm volatile("" : "+v"(m), "+v"(igw));  // no value of the slot live across its reload
+        // no value of the slot live across its reload (igw only with ignore bytes: otherwise it is
+        // the constant ~0 and the masks below fold away)
+        if (IGN) asm volatile("" : "+v"(m), "+v"(igw));
+        else asm volatile("" : "+v"(m));
         const bool mine = q < nmine;
         const int sl = (int)(t % RING);
         KBZ_STAMP(1);
@@ -1552,18 +1561,18 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
             __builtin_amdgcn_s_sleep(1);
         asm volatile("" ::: "memory");
         KBZ_STAMP(2);
+        if (mine) {  // wave-uniform: one branch around the tile's mixes and ring writes
 #pragma unroll
-        for (int i = 0; i < NLD; i++) {
-          const int rr = RPI * i + lr;
-          const int idx = sl * TILE + rr * SLOTS + (ls ^ (rr & 15));
-          const u32x4 c = R[u][i];
-          const uint64_t c0 = (uint64_t)c.x | ((uint64_t)c.y << 32);
-          const uint64_t c1 = (uint64_t)c.z | ((uint64_t)c.w << 32);
-          const uint64_t g0 = (uint64_t)igw.x | ((uint64_t)igw.y << 32);
-          const uint64_t g1 = (uint64_t)igw.z | ((uint64_t)igw.w << 32);
-          const uint64_t k0 = (KBZ_PASS1D_ABL & 8) ? c0 & g0 : h32_mix_mad(c0 & g0);
-          const uint64_t k1 = (KBZ_PASS1D_ABL & 8) ? c1 & g1 : h32_mix_mad(c1 & g1);
-          if (mine) {
+          for (int i = 0; i < NLD; i++) {
+            const int rr = RPI * i + lr;
+            const int idx = sl * TILE + rr * SLOTS + (ls ^ (rr & 15));
+            const u32x4 c = R[u][i];
+            const uint64_t c0 = (uint64_t)c.x | ((uint64_t)c.y << 32);
+            const uint64_t c1 = (uint64_t)c.z | ((uint64_t)c.w << 32);
+            const uint64_t g0 = (uint64_t)igw.x | ((uint64_t)igw.y << 32);
+            const uint64_t g1 = (uint64_t)igw.z | ((uint64_t)igw.w << 32);
+            const uint64_t k0 = (KBZ_PASS1D_ABL & 8) ? c0 & g0 : h32_mix_mad(c0 & g0);
+            const uint64_t k1 = (KBZ_PASS1D_ABL & 8) ? c1 & g1 : h32_mix_mad(c1 & g1);
             kring[idx] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1,
                                     (uint32_t)(k1 >> 32));
             if (IGN) {  // the neighbour test looks at the bytes whose ignore byte is 0
