@@ -292,6 +292,33 @@ def live_traffic(args, warmup=1, steps=4):
                       f"{med(write) * 1024:.0f} B"}
 
 
+VALU_ISSUE_CYCLES = 4  # one wave64 integer VALU instruction per SIMD per 4 cycles (tools/xprobe,
+                       # SQ_ACTIVE_INST_VALU = SQ_INSTS_VALU quad-cycles: profiles/r03_v8)
+SIMDS = 256 * 4
+CLOCK_PEAK_GHZ = 2.4
+
+
+def live_valu(args, warmup=1, steps=2):
+    """Config 3's pass 1 is VALU-issue-bound, not HBM-bound: the VALU instructions of one launch
+    (SQ_INSTS_VALU, all waves) and the time they take if all 1,024 SIMDs issued one every 4
+    cycles at the peak clock -- the instruction-count floor the kernel is measured against."""
+    import tempfile
+
+    wa = ["--workload", args.workload, "--mode", args.mode, "--batch", str(args.batch),
+          "--map-size", str(args.map_size), "--warmup", str(warmup), "--steps", str(steps),
+          "--seed", str(args.seed), *(["--hash"] if args.hash else [])]
+    with tempfile.TemporaryDirectory() as d:
+        v = _pmc_pass("SQ_INSTS_VALU", wa, os.path.join(d, "v"))[warmup:]
+    if not v:
+        return None
+    inst = sorted(v)[len(v) // 2]
+    floor_ms = inst * VALU_ISSUE_CYCLES / SIMDS / (CLOCK_PEAK_GHZ * 1e6)
+    return {"instructions_per_launch": inst, "floor_ms": round(floor_ms, 4),
+            "what": f"SQ_INSTS_VALU (live rocprofv3 --pmc, median of {len(v)} fresh-batch "
+                    f"dispatches) x {VALU_ISSUE_CYCLES} cycles / {SIMDS} SIMDs at "
+                    f"{CLOCK_PEAK_GHZ} GHz"}
+
+
 def merge_traffic(args, warmup=1, steps=3):
     """HBM bytes of one local AND-fold of the merge leg (k_and_groups tree + k_and_rows), from
     PMC like live_traffic: the fold kernels' per-dispatch FETCH_SIZE x2 + WRITE_SIZE summed over
@@ -520,6 +547,19 @@ def main_triage(args):
             traffic = {"bytes": None, "source": f"live PMC failed: {type(e).__name__}"}
     if traffic is None:
         traffic = stored_traffic(args.workload) or {"bytes": None, "source": "none"}
+    valu = None
+    if rank == 0 and world == 1 and args.pmc and dense:
+        try:
+            valu = live_valu(args)
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal
+            valu = {"instructions_per_launch": None, "what": f"live PMC failed: {type(e).__name__}"}
+    wide = B < 512 * 64
+    if mode == MODES["dynamorio"]:
+        kname = "k_pass1d" if wide else "k_pass1s"
+    elif want:
+        kname = "k_pass1w" if wide else "k_pass1s"
+    else:
+        kname = "k_pass1n (wide)" if wide else "k_pass1n"
     res = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -547,13 +587,16 @@ def main_triage(args):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic["bytes"], "traffic_source": traffic["source"],
-                     "kernel": ("k_pass1s" if want else "k_pass1n") if B >= 512 * 64
-                               else ("k_pass1w" if want else "k_pass1n (wide)"),
+                     "kernel": kname,
                      "avg_launch_ms": round(pass1_ms, 4),
                      "algorithmic_bytes_per_launch": B * M},
         "pass1_share_of_step": round(pass1_ms / ms_per_step, 4),
         "variants": variants,
     }
+    if valu and valu.get("instructions_per_launch"):
+        valu["frac"] = round(valu["floor_ms"] / pass1_ms, 4)
+        valu["bound"] = "valu"
+        res["roofline"]["valu_issue"] = valu
     if world > 1:
         # attribution of a sub-linear curve: every rank's pass-1 time and the time its steps
         # spent in the all-gathers (HIP events around each phase of the timed steps)

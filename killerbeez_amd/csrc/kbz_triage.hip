@@ -1911,10 +1911,14 @@ __device__ __forceinline__ void flush_items(ItemStage &st, uint64_t *items, uint
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the area is reused
   st.n = 0;
 }
+#ifndef KBZ_WIN_ITEMS  // claimed bytes of one chunk's 1-KiB column window from which k_resolve
+#define KBZ_WIN_ITEMS 16  // streams the window's 64 rows (64 KiB, coalesced) instead of reading
+#endif                    // one scattered byte per row and claimed byte
 __device__ __forceinline__ void emit_items_wave(uint32_t chunk, int k, uint32_t col, uint4 nb,
                                                 uint4 vir, uint4 prev, ItemStage &st,
                                                 uint64_t *items, uint32_t cap,
-                                                uint32_t *counters) {
+                                                uint32_t *counters, uint8_t *win_prev,
+                                                bool live) {
   const uint32_t w[4] = {nb.x, nb.y, nb.z, nb.w};
   const uint32_t vv[4] = {vir.x, vir.y, vir.z, vir.w};
   const uint32_t pv[4] = {prev.x, prev.y, prev.z, prev.w};
@@ -1923,6 +1927,17 @@ __device__ __forceinline__ void emit_items_wave(uint32_t chunk, int k, uint32_t 
   for (int i = 0; i < 4; i++) cnt += __popc(nonzero_bytes8(w[i]) & 0x80808080u);
   uint32_t total;
   const uint32_t off = wave_excl_prefix(cnt, total);
+  if (total >= KBZ_WIN_ITEMS) {
+    // window item (new bits field 0): the wave's 1-KiB column window of this chunk.  The running
+    // OR before this chunk replaces the chunk's (consumed) column OR in chunk_or, and k_resolve
+    // re-derives the claims row by row in order: new bits of row r = t_r & V & ~(prev | rows < r)
+    if (live) *(uint4 *)win_prev = prev;
+    const uint32_t wcol = __shfl(col, 0);
+    if (st.n + 1 > kWaveItems) flush_items(st, items, cap, counters);
+    if ((threadIdx.x & 63) == 0) st.buf[st.n] = pack_item(chunk, k, wcol, 0u, false);
+    st.n += 1;
+    return;
+  }
   if (st.n + total > kWaveItems) flush_items(st, items, cap, counters);
   const bool staged = total <= kWaveItems;  // else (rare) straight to the global list
   uint32_t base = st.n + off;
@@ -1953,7 +1968,7 @@ __device__ __forceinline__ void emit_items_wave(uint32_t chunk, int k, uint32_t 
 // A segment whose cumulative OR (segprev of the next segment, or this shard's total for the
 // last one) adds no still-virgin bit over `prev` cannot claim anything: its waves skip the
 // chunk walk (exact; in steady-state fuzzing almost every segment takes this path).
-__global__ __launch_bounds__(256) void k_scan(const uint8_t *chunk_or, const uint8_t *chunk_cls,
+__global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *chunk_cls,
                                                uint32_t nchunks, uint32_t seg_len, int nclass,
                                                uint32_t map_size, const uint8_t *segprev,
                                                uint32_t nseg, const uint8_t *ltotal,
@@ -2036,7 +2051,8 @@ __global__ __launch_bounds__(256) void k_scan(const uint8_t *chunk_or, const uin
         const uint4 nb = make_uint4(o[u].x & vr.x & ~prev.x, o[u].y & vr.y & ~prev.y,
                                     o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
         if (__ballot(nb.x | nb.y | nb.z | nb.w))  // wave-uniform: all lanes join the prefix
-          emit_items_wave(c, k, col, nb, vir, prev, stg, items, cap, counters);
+          emit_items_wave(c, k, col, nb, vir, prev, stg, items, cap, counters,
+                          (uint8_t *)chunk_or + (size_t)c * nclass * map_size + kc, live);
         prev = or4(prev, o[u]);
       }
     }
@@ -2044,11 +2060,83 @@ __global__ __launch_bounds__(256) void k_scan(const uint8_t *chunk_or, const uin
   flush_items(stg, items, cap, counters);
 }
 
+// Window item: lane l owns 16-B column group l of the chunk's 1-KiB window; the rows of the
+// chunk that belong to class k (and are not skipped) are walked in order with their running OR
+// `acc`: row r claims t_r & V & ~(prev | acc) (has_new_bits, afl_instrumentation.c:600-662, over
+// the window), and scores 2 if it is the first row with a nonzero byte where V is 0xff and prev
+// is 0 (:644-651).  Rows are loaded 8 at a time (1 KiB per row, coalesced).
+__device__ __forceinline__ void resolve_window(const uint8_t *traces, size_t stride, uint32_t n,
+                                               int mode, const int8_t *outcome,
+                                               const uint8_t *skip, uint32_t chunk, int k,
+                                               uint32_t wcol, const uint8_t *win_prev,
+                                               const uint8_t *vcur, const uint8_t *ignore,
+                                               uint32_t map_size, uint32_t *hnb32,
+                                               uint32_t *err) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t row0 = (uint64_t)chunk * kChunk;
+  const uint64_t rl = row0 + lane;
+  bool ok = rl < n;
+  if (ok && outcome) ok = class_of(mode, outcome[rl]) == k;
+  if (ok && skip) ok = !skip[rl];
+  uint64_t rows = __ballot(ok);
+  const uint32_t col = wcol + 16 * lane;
+  const bool live = col < map_size;
+  const uint32_t cl = live ? col : wcol;
+  const uint4 prev = *(const uint4 *)(win_prev + (cl - wcol));  // k_scan's running OR
+  const uint4 vir = *(const uint4 *)(vcur + (size_t)k * map_size + cl);
+  uint64_t rel0 = ~0ull, rel1 = ~0ull;
+  if (ignore) {
+    const uint4 ig = *(const uint4 *)(ignore + cl);
+    rel0 = ~nonzero_bytes8((uint64_t)ig.x | ((uint64_t)ig.y << 32));
+    rel1 = ~nonzero_bytes8((uint64_t)ig.z | ((uint64_t)ig.w << 32));
+  }
+  uint64_t vr0 = ((uint64_t)vir.x | ((uint64_t)vir.y << 32)) & rel0;
+  uint64_t vr1 = ((uint64_t)vir.z | ((uint64_t)vir.w << 32)) & rel1;
+  if (!live) vr0 = vr1 = 0;
+  // bytes with V == 0xff (examined): a 2 is possible there while prev | acc is still 0
+  const uint64_t ff0 = ~nonzero_bytes8(~vr0), ff1 = ~nonzero_bytes8(~vr1);
+  uint64_t pa0 = (uint64_t)prev.x | ((uint64_t)prev.y << 32);
+  uint64_t pa1 = (uint64_t)prev.z | ((uint64_t)prev.w << 32);
+  const int xf = class_xf(mode, k);
+  bool claimed = false;
+  while (rows) {
+    int rr[8];
+    uint4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {  // up to 8 rows' loads in flight
+      rr[u] = rows ? __builtin_ctzll(rows) : -1;
+      rows &= rows - 1;
+      const uint64_t r = row0 + (rr[u] >= 0 ? rr[u] : 0);
+      v[u] = *(const uint4 *)(traces + r * stride + cl);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      if (rr[u] < 0) break;  // wave-uniform
+      const uint64_t t0 = xform8((uint64_t)v[u].x | ((uint64_t)v[u].y << 32), xf) & rel0;
+      const uint64_t t1 = xform8((uint64_t)v[u].z | ((uint64_t)v[u].w << 32), xf) & rel1;
+      const bool nw = ((t0 & vr0 & ~pa0) | (t1 & vr1 & ~pa1)) != 0;
+      const bool two = ((nonzero_bytes8(t0) & ff0 & ~nonzero_bytes8(pa0)) |
+                        (nonzero_bytes8(t1) & ff1 & ~nonzero_bytes8(pa1))) != 0;
+      pa0 |= t0;
+      pa1 |= t1;
+      const uint32_t sc = __ballot(two) ? 2u : __ballot(nw) ? 1u : 0u;
+      if (sc) {
+        claimed = true;
+        if (lane == 0) atomicMax(&hnb32[row0 + rr[u]], sc);
+      }
+    }
+  }
+  if (!claimed && lane == 0) atomicOr(err, 2u);  // k_scan saw new bits here: inconsistent
+}
+
 __global__ __launch_bounds__(256) void k_resolve(const uint8_t *traces, size_t stride, uint32_t n,
                                                   int mode, const int8_t *outcome,
                                                   const uint8_t *skip, const uint64_t *items,
                                                   const uint32_t *counters, uint32_t cap,
-                                                  uint32_t *hnb32, uint32_t *err) {
+                                                  uint32_t *hnb32, uint32_t *err,
+                                                  const uint8_t *chunk_or, int nclass,
+                                                  uint32_t map_size, const uint8_t *vcur,
+                                                  const uint8_t *ignore) {
   const int lane = threadIdx.x & 63;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -2060,6 +2148,12 @@ __global__ __launch_bounds__(256) void k_resolve(const uint8_t *traces, size_t s
     const int k = (item >> 9) & 3;
     const uint32_t col = (item >> 11) & 0xffffff;
     const uint32_t chunk = (uint32_t)(item >> 35);
+    if (nb == 0) {  // window item (wave-uniform)
+      resolve_window(traces, stride, n, mode, outcome, skip, chunk, k, col,
+                     chunk_or + ((size_t)chunk * nclass + k) * map_size + col, vcur, ignore,
+                     map_size, hnb32, err);
+      continue;
+    }
     const uint64_t row = (uint64_t)chunk * kChunk + lane;
     const uint64_t rc = min(row, (uint64_t)n - 1);  // independent loads, one round trip
     const int oc = outcome ? outcome[rc] : KBZ_FUZZ_NONE;
@@ -3080,7 +3174,8 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
     hipLaunchKernelGGL(k_resolve, dim3(512), dim3(256), 0, s, c->cur_traces, c->cur_stride,
                        (uint32_t)c->cur_n, c->mode, c->cur_outcome,
                        c->mode == KBZ_MODE_DYNAMORIO ? c->skip : nullptr, c->items, c->counters,
-                       c->item_cap, c->hnb32, c->counters + 2);
+                       c->item_cap, c->hnb32, c->counters + 2, c->chunk_or, c->nc,
+                       (uint32_t)c->M, c->V[c->vcur], ign);
     HIP_TRY(hipGetLastError());
     if (stage_end(c, s, KBZ_STAGE_RESOLVE, st0)) return -1;
     if (stage_begin(c, s, &st0)) return -1;
