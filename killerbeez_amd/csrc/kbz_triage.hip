@@ -1918,7 +1918,7 @@ __device__ __forceinline__ void emit_items_wave(uint32_t chunk, int k, uint32_t 
                                                 uint4 vir, uint4 prev, ItemStage &st,
                                                 uint64_t *items, uint32_t cap,
                                                 uint32_t *counters, uint8_t *win_prev,
-                                                bool live) {
+                                                bool live, uint32_t win_items) {
   const uint32_t w[4] = {nb.x, nb.y, nb.z, nb.w};
   const uint32_t vv[4] = {vir.x, vir.y, vir.z, vir.w};
   const uint32_t pv[4] = {prev.x, prev.y, prev.z, prev.w};
@@ -1927,7 +1927,7 @@ __device__ __forceinline__ void emit_items_wave(uint32_t chunk, int k, uint32_t 
   for (int i = 0; i < 4; i++) cnt += __popc(nonzero_bytes8(w[i]) & 0x80808080u);
   uint32_t total;
   const uint32_t off = wave_excl_prefix(cnt, total);
-  if (total >= KBZ_WIN_ITEMS) {
+  if (total >= win_items) {
     // window item (new bits field 0): the wave's 1-KiB column window of this chunk.  The running
     // OR before this chunk replaces the chunk's (consumed) column OR in chunk_or, and k_resolve
     // re-derives the claims row by row in order: new bits of row r = t_r & V & ~(prev | rows < r)
@@ -1977,7 +1977,7 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
                                                const uint8_t *ignore, uint64_t *items,
                                                uint32_t cap, uint32_t *counters,
                                                const uint64_t *tflags, uint32_t nfw,
-                                               const uint32_t *listed) {
+                                               const uint32_t *listed, uint32_t win_items) {
   // no per-lane early return: every lane of a wave takes part in the item-allocation prefix
   const uint32_t col0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
   const bool live = col0 < map_size;
@@ -2052,7 +2052,8 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
                                     o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
         if (__ballot(nb.x | nb.y | nb.z | nb.w))  // wave-uniform: all lanes join the prefix
           emit_items_wave(c, k, col, nb, vir, prev, stg, items, cap, counters,
-                          (uint8_t *)chunk_or + (size_t)c * nclass * map_size + kc, live);
+                          (uint8_t *)chunk_or + (size_t)c * nclass * map_size + kc, live,
+                          win_items);
         prev = or4(prev, o[u]);
       }
     }
@@ -2479,6 +2480,7 @@ struct kbz_ctx {
   uint8_t *total = nullptr;
   uint64_t *items = nullptr;
   uint32_t item_cap = 0;
+  uint32_t win_items = KBZ_WIN_ITEMS;  // claimed bytes per chunk x 1-KiB window: window item
   uint32_t *counters = nullptr;  // [0] items, [1] overflow, [2] resolve error, [3] fix list,
                                  // [4] bad rows, [6..7] clean flags of the saved rows,
                                  // [8..10] the last finished batch's [0], [3], [4]
@@ -2789,6 +2791,8 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   // tests only: a smaller claim list, to exercise the overflow error path (a real batch cannot
   // overflow it: each column yields at most 8 items per map per batch)
   if (const char *cap = getenv("KBZ_DEBUG_ITEM_CAP")) c->item_cap = std::max(1, atoi(cap));
+  // tests only: force window items everywhere (1) or never (a large value)
+  if (const char *w = getenv("KBZ_DEBUG_WIN_ITEMS")) c->win_items = (uint32_t)std::max(1, atoi(w));
   bool ok = !dalloc(&c->V[0], 3 * M) && !dalloc(&c->V[1], 3 * M) && !dalloc(&c->last, 2) &&
             !dalloc(&c->chunk_or, c->max_chunks * nc * M) && !dalloc(&c->chunk_cls, c->max_chunks) &&
             !dalloc(&c->tflags, c->max_chunks * nc * c->nfw) &&
@@ -3166,7 +3170,7 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
                      c->cur_chunks, c->cur_seg_len, c->nc, (uint32_t)c->M, c->segprev, nseg,
                      c->total, prefix, total, c->V[c->vcur], c->V[vn], ign, c->items,
                      c->item_cap, c->counters, c->tflags, c->nfw,
-                     c->mode == KBZ_MODE_DYNAMORIO ? c->flags : nullptr);
+                     c->mode == KBZ_MODE_DYNAMORIO ? c->flags : nullptr, c->win_items);
   HIP_TRY(hipGetLastError());
   if (stage_end(c, s, KBZ_STAGE_SCAN, st0)) return -1;
   if (c->cur_n) {

@@ -741,3 +741,33 @@ def test_claim_overflow_is_reported_once(gpu, monkeypatch):
         rows = np.stack([t[200], one[0], t[201]])[:j + 1]
         exp = oracle.triage_batch(MODE_AFL, rows, np.zeros(j + 1, np.int8), virgin=vm)
         assert p.result(tk) == exp["hnb"][j]
+
+
+@pytest.mark.parametrize("win", ["1", "16", "1000000"], ids=["all-windows", "default", "no-windows"])
+@pytest.mark.parametrize("mode", MODES)
+def test_claims_window_and_byte_items(gpu, mode, win, monkeypatch):
+    """The two claim paths of k_resolve give identical results: per-byte items (one scattered
+    byte of each of the chunk's rows) and window items (the chunk's 1-KiB column window streamed
+    row by row in order).  Fresh virgin maps and dense rows make windows with hundreds of
+    claimed bytes, sparse rows windows with one or two; a 4,864-B map leaves lanes of its last window
+    past the end; partial last chunk; DynamoRIO with ignore bytes and repeated execs (skipped
+    rows must not claim), AFL with hangs/crashes (simplified classes: every byte claims)."""
+    monkeypatch.setenv("KBZ_DEBUG_WIN_ITEMS", win)
+    rng = np.random.default_rng(int(win) % 97 + mode)
+    for m, n in [(65536, 700), (19 * 256, 200), (1 << 20, 70)]:
+        t = synth.uniform_np(n, m, seed=m + n, density=0.3)
+        t[: n // 3] = synth.uniform_np(n // 3, m, seed=m - n, density=0.01)
+        oc = rng.choice(3, size=n, p=[0.8, 0.1, 0.1]).astype(np.int8)
+        ign = None
+        if mode == MODE_DYNAMORIO:
+            ign = np.where(rng.random(m) < 0.7, 0, rng.integers(1, 256, size=m)).astype(np.uint8)
+            for j in rng.integers(1, n, n // 4):
+                t[j] = t[j - 1]                # skipped rows (same hash): never claim
+        ctx = TriageContext(m, mode, n)
+        if ign is not None:
+            ctx.set_ignore(ign)
+        exp = check(mode, t, oc, ignore=ign, ctx=ctx)
+        assert exp["hnb"].max() == 2
+        t2 = synth.uniform_np(n, m, seed=m + 2 * n, density=0.3)
+        check(mode, t2, oc, ignore=ign, ctx=ctx)  # carried maps: fewer, scattered claims
+        ctx.close()
