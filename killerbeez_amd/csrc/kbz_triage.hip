@@ -268,6 +268,12 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #ifndef KBZ_SROWS_MAX
 #define KBZ_SROWS_MAX 16  // 8, 16, 32 equal at 2 % hangs + crashes; 4 is slower (profiles/r02_v19)
 #endif
+#ifndef KBZ_PASS1_LMIX4  // k_pass1s wave L: mixes of 4 words at once, ahead of their chain steps
+#define KBZ_PASS1_LMIX4 0  // 1: 0.83 vs 0.80 ms (VALU), profiles/r03_v10
+#endif
+#ifndef KBZ_PASS1_TPRE  // k_pass1s wave T: LDS slots read this many slots ahead (1 or 4)
+#define KBZ_PASS1_TPRE 4
+#endif
 #ifndef KBZ_PASS1_TMIX  // timing variants: 0 = wave L mixes in every mode
 #define KBZ_PASS1_TMIX 1
 #endif
@@ -328,7 +334,8 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   // LDS for wave L (T only simplifies the few hang/crash rows there, L was the slower wave:
   // pass 1 1.23 -> 1.13 ms, profiles/r02_v18).  DynamoRIO and AFL_CLASSIFY keep the mix on L:
   // T's classify makes T the busier wave there.  XXH64 needs the transformed words on L.
-  constexpr bool TMIX = KBZ_PASS1_TMIX && MODE == KBZ_MODE_AFL && !X64;
+  // KBZ_PASS1_TMIX == 2: T mixes in every mode (then wave L is a bare chain).
+  constexpr bool TMIX = KBZ_PASS1_TMIX == 2 ? !X64 : (KBZ_PASS1_TMIX && MODE == KBZ_MODE_AFL && !X64);
   // AFL modes: the simplified classes' column ORs come from their rows, once per tile
   constexpr bool SROWS = KBZ_PASS1_SROWS && NC > 1;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = 8;  // 8 x 1-KiB loads per wave per tile
@@ -397,6 +404,39 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         // software pipeline: the next two slots are in flight while these 4 words chain
         const int qn = (q + 2) & (SLOTS - 1);
         const uint4 n0 = row[qn ^ sw], n1 = row[(qn + 1) ^ sw];
+        if (KBZ_PASS1_LMIX4 && !TMIX) {
+          // the 4 words' mixes are independent of the chain: computed together, ahead of the 4
+          // steps (one ballot per group; h32_mix(0) = 0), so the chain waits on no mix
+          const uint64_t wv[4] = {ld_u64(v0, 0), ld_u64(v0, 1), ld_u64(v1, 0), ld_u64(v1, 1)};
+          uint64_t tv[4], kv[4];
+          if (__ballot((wv[0] | wv[1] | wv[2] | wv[3]) != 0)) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+              tv[j] = (simp && wv[j] == 0) ? kSimpleZero : wv[j];
+              kv[j] = h32_mix_mad(tv[j] & (IGN ? ig[2 * q + j] : ~0ull));
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+              tv[j] = simp ? kSimpleZero : 0;
+              kv[j] = simp ? ksimp : 0;
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            h = h32_step_fast(h, kv[j]);
+            if (X64) {
+              const int xl = j & 3;
+              if (xl == 0) x0 = xx_round(x0, tv[j]);
+              else if (xl == 1) x1 = xx_round(x1, tv[j]);
+              else if (xl == 2) x2 = xx_round(x2, tv[j]);
+              else x3 = xx_round(x3, tv[j]);
+            }
+          }
+          v0 = n0;
+          v1 = n1;
+          continue;
+        }
 #pragma unroll
         for (int qq = 0; qq < 2; qq++) {
           const uint4 v = qq ? v1 : v0;
@@ -541,12 +581,18 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
       }
       uint4 *row = &lds[b * TILE + lane * SLOTS];
       const int sw = lane & 15;
-      uint4 vnext = row[0 ^ sw];
-#pragma unroll 2
-      for (int q = 0; q < ((ABL & 1) ? 0 : SLOTS); q++) {
+      constexpr int TP = KBZ_PASS1_TPRE;  // slots in flight: a mostly-zero slot takes a few
+      uint4 vring[TP];                    // instructions, far less than an LDS round trip
+#pragma unroll
+      for (int j = 0; j < TP; j++) vring[j] = row[j ^ sw];
+#pragma unroll 1
+      for (int q0 = 0; q0 < ((ABL & 1) ? 0 : SLOTS); q0 += TP)
+#pragma unroll
+      for (int u = 0; u < TP; u++) {
+        const int q = q0 + u;
         uint4 *slot = &row[q ^ sw];
-        uint4 v = vnext;
-        vnext = row[((q + 1) & (SLOTS - 1)) ^ sw];  // next slot in flight meanwhile
+        uint4 v = vring[u];
+        vring[u] = row[((q + TP) & (SLOTS - 1)) ^ sw];  // (wraps at the end: discarded)
         bool dirty = false;
 #pragma unroll
         for (int e = 0; e < 2; e++) {
@@ -554,7 +600,8 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
           const uint64_t x = ld_u64(v, e);
           if (__ballot(x != 0)) {
             const uint64_t tw = xform8(x, xf);
-            const uint64_t out = TMIX ? h32_mix(tw) : tw;  // what wave L chains next step
+            // what wave L chains next step (with ignore bytes the mix sees the kept bytes only)
+            const uint64_t out = TMIX ? h32_mix_mad(tw & (IGN ? ig[wi] : ~0ull)) : tw;
             if (e) { v.z = (uint32_t)out; v.w = (uint32_t)(out >> 32); }
             else { v.x = (uint32_t)out; v.y = (uint32_t)(out >> 32); }
             dirty = true;
