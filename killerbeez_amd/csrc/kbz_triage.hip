@@ -272,7 +272,7 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #define KBZ_PASS1_LMIX4 0  // 1: 0.83 vs 0.80 ms (VALU), profiles/r03_v10
 #endif
 #ifndef KBZ_PASS1_TPRE  // k_pass1s wave T: LDS slots read this many slots ahead (1 or 4)
-#define KBZ_PASS1_TPRE 4
+#define KBZ_PASS1_TPRE 8  // 1 / 4 / 8: 0.80 / 0.767 / 0.744 ms, profiles/r03_v10
 #endif
 #ifndef KBZ_PASS1_TMIX  // timing variants: 0 = wave L mixes in every mode
 #define KBZ_PASS1_TMIX 1
