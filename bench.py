@@ -292,6 +292,8 @@ def live_traffic(args, warmup=1, steps=4):
                       f"{med(write) * 1024:.0f} B"}
 
 
+# A/B only: KBZ_BENCH_P1_TIMING=0 times the steps without the pass-1 events (roofline invalid)
+P1_TIMING = os.environ.get("KBZ_BENCH_P1_TIMING", "1") != "0"
 VALU_ISSUE_CYCLES = 4  # one wave64 integer VALU instruction per SIMD per 4 cycles (tools/xprobe,
                        # SQ_ACTIVE_INST_VALU = SQ_INSTS_VALU quad-cycles: profiles/r03_v8)
 SIMDS = 256 * 4
@@ -476,7 +478,7 @@ def main_triage(args):
         events per stage) stays off here: it adds ~50 us per step; the warmup steps time stages."""
         barrier_sync(world, dev)
         ctx.sync()
-        ctx.time_pass1(True)
+        ctx.time_pass1(P1_TIMING)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         t0 = time.perf_counter()
         ev[0].record()
@@ -487,7 +489,7 @@ def main_triage(args):
         el = time.perf_counter() - t0
         ms, launches = ctx.time_pass1(False)
         ctx.sync()
-        r = (max_over_ranks(el, world, dev), ms / max(1, launches))
+        r = (max_over_ranks(el, world, dev), ms / launches if launches else float("nan"))
         return r + (ev[0].elapsed_time(ev[1]),) if events else r
 
     # warmup on fresh batches (the first one on all-0xff virgin maps, timed by itself); the

@@ -22,6 +22,7 @@
 //   resolve one wave per item re-reads that column of the claiming chunk's 64 rows and
 //           finds, per new bit, the first trace holding it -> atomicMax(hnb, 1 or 2).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -1944,8 +1945,12 @@ struct ItemStage {
   uint64_t *buf;  // this wave's LDS staging area, kWaveItems entries
   uint32_t n;     // wave-uniform fill
 };
+#ifndef KBZ_SCAN_ABL  // timing-only ablations (wrong results): 1 = no claim items, 2 = items
+#define KBZ_SCAN_ABL 0   // staged but never appended to the global list
+#endif
 __device__ __forceinline__ void flush_items(ItemStage &st, uint64_t *items, uint32_t cap,
                                             uint32_t *counters) {
+  if (KBZ_SCAN_ABL & 2) st.n = 0;
   if (!st.n) return;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's staged writes are done
   uint32_t base = 0;
@@ -2032,18 +2037,36 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
   const uint32_t s = blockIdx.y;
   const int k = blockIdx.z;
   const size_t kc = (size_t)k * map_size + col;
-  uint4 prev = *(const uint4 *)(segprev + (size_t)s * nclass * map_size + kc);
-  if (gprefix) prev = or4(prev, *(const uint4 *)(gprefix + kc));
+  // every load of the prologue in one round trip (absent inputs read a valid dummy and are
+  // masked): the compiler otherwise waits for each before issuing the next
+  const uint4 p0 = *(const uint4 *)(segprev + (size_t)s * nclass * map_size + kc);
+  const uint4 p1 = *(const uint4 *)((gprefix ? gprefix : segprev) + kc);
   const uint4 vir = *(const uint4 *)(vcur + kc);
+  const uint4 ig = *(const uint4 *)((ignore ? ignore : vcur) + col);
+  const uint4 tot = *(const uint4 *)(gtotal + kc);
+  const uint4 send = *(const uint4 *)((s + 1 < nseg) ? segprev + (size_t)(s + 1) * nclass * map_size + kc
+                                                      : ltotal + kc);
+  const uint32_t c0 = s * seg_len, c1 = min(nchunks, c0 + seg_len);
+  const uint32_t t0 = (blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * 16 / kTileW;
+  // the first 64 chunks' tile flags, for the walk below (also in this round trip)
+  const uint32_t cl0 = c0 + (threadIdx.x & 63);
+  uint8_t ccls0 = 0;
+  uint64_t tfw0 = 0;
+  uint32_t lst0 = 0;
+  if (cl0 < c1) {
+    ccls0 = chunk_cls[cl0];
+    tfw0 = tflags[((size_t)cl0 * nclass + k) * nfw + (t0 >> 6)];
+    if (listed) lst0 = listed[cl0];
+  }
+  uint4 prev = gprefix ? or4(p0, p1) : p0;
   uint4 rel = make_uint4(~0u, ~0u, ~0u, ~0u);
   if (ignore) {  // has_new_bits_with_ignore only examines bytes whose ignore byte is 0
-    const uint4 ig = *(const uint4 *)(ignore + col);
     const uint64_t m0 = nonzero_bytes8((uint64_t)ig.x | ((uint64_t)ig.y << 32));
     const uint64_t m1 = nonzero_bytes8((uint64_t)ig.z | ((uint64_t)ig.w << 32));
     rel = make_uint4(~(uint32_t)m0, ~(uint32_t)(m0 >> 32), ~(uint32_t)m1, ~(uint32_t)(m1 >> 32));
   }
   if (s == 0 && live) {
-    const uint4 t = *(const uint4 *)(gtotal + kc);
+    const uint4 t = tot;
     *(uint4 *)(vnext + kc) = make_uint4(vir.x & ~(t.x & rel.x), vir.y & ~(t.y & rel.y),
                                         vir.z & ~(t.z & rel.z), vir.w & ~(t.w & rel.w));
     if (k == nclass - 1)  // maps this mode does not use (DynamoRIO: tmout, crash) carry over
@@ -2055,22 +2078,20 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
                         : make_uint4(0, 0, 0, 0);
   __shared__ uint64_t stage_buf[4][kWaveItems];  // 256 threads = 4 waves
   ItemStage stg{stage_buf[threadIdx.x >> 6], 0u};
-  const uint4 send = *(const uint4 *)((s + 1 < nseg) ? segprev + (size_t)(s + 1) * nclass * map_size + kc
-                                                      : ltotal + kc);
   const uint32_t seg_new = (send.x & vr.x & ~prev.x) | (send.y & vr.y & ~prev.y) |
                            (send.z & vr.z & ~prev.z) | (send.w & vr.w & ~prev.w);
   if (!__ballot(seg_new != 0)) return;  // wave-uniform: nothing new in this segment
-  const uint32_t c0 = s * seg_len, c1 = min(nchunks, c0 + seg_len);
   // Only chunks that hold traces of class k AND stored (or, DynamoRIO fix path, recomputed) one
   // of this wave's 4 tiles can add bits here: an unstored tile held no still-virgin bit, so a
   // skipped chunk changes neither the claims nor the running OR.  Lane l tests chunk cg + l;
   // the wave walks the set bits of the ballot in order, KBZ_SCAN_ILP chunk loads per memory round
   // trip.
-  const uint32_t t0 = (blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * 16 / kTileW;
   for (uint32_t cg = c0; cg < c1; cg += 64) {
     const uint32_t cl = cg + (threadIdx.x & 63);
     bool any = false;
-    if (cl < c1 && ((chunk_cls[cl] >> k) & 1))
+    if (cg == c0) {  // loaded with the prologue
+      if (cl < c1 && ((ccls0 >> k) & 1)) any = lst0 || ((tfw0 >> (t0 & 63)) & 0xFull);
+    } else if (cl < c1 && ((chunk_cls[cl] >> k) & 1))
       any = (listed && listed[cl]) ||
             ((tflags[((size_t)cl * nclass + k) * nfw + (t0 >> 6)] >> (t0 & 63)) & 0xFull);
     uint64_t mask = __ballot(any);
@@ -2097,7 +2118,7 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
         if (!st[u]) o[u] = make_uint4(0, 0, 0, 0);  // nothing still virgin in that tile
         const uint4 nb = make_uint4(o[u].x & vr.x & ~prev.x, o[u].y & vr.y & ~prev.y,
                                     o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
-        if (__ballot(nb.x | nb.y | nb.z | nb.w))  // wave-uniform: all lanes join the prefix
+        if (!(KBZ_SCAN_ABL & 1) && __ballot(nb.x | nb.y | nb.z | nb.w))  // wave-uniform
           emit_items_wave(c, k, col, nb, vir, prev, stg, items, cap, counters,
                           (uint8_t *)chunk_or + (size_t)c * nclass * map_size + kc, live,
                           win_items);
@@ -2685,6 +2706,20 @@ void launch_abl(int depth, const Pass1Args &a, uint32_t chunks, hipStream_t s) {
   else hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, ABL, 4>), dim3(chunks), dim3(128), 0, s, a);
 }
 #endif
+// Pass-1 launches.  With timing on (kbz_ctx_time_pass1) the kernel is dispatched by
+// hipExtLaunchKernelGGL with start/stop events taken from its own dispatch packet: no marker
+// packets around it (two hipEventRecord calls left ~6 us of idle GPU each between pass 1 and
+// its neighbours, ~1.5 % of a config-2 step, profiles/r03_v8 kernel trace).
+struct P1Ev {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+template <typename K>
+void p1_launch(K kernel, dim3 grid, dim3 block, hipStream_t s, const P1Ev &ev, const Pass1Args &a) {
+  if (ev.start)
+    hipExtLaunchKernelGGL(kernel, grid, block, 0, s, ev.start, ev.stop, 0, a);
+  else
+    hipLaunchKernelGGL(kernel, grid, block, 0, s, a);
+}
 #ifndef KBZ_PASS1D  // timing-only A/B builds: 0 = the lock-step k_pass1w for wide DynamoRIO batches
 #define KBZ_PASS1D 1
 #endif
@@ -2698,12 +2733,13 @@ void launch_abl(int depth, const Pass1Args &a, uint32_t chunks, hipStream_t s) {
 #define KBZ_PASS1D_NX 6  // 10 X waves with D = 1 (3 per SIMD): 3.72-3.77 vs 3.54 ms (r03_v7)
 #endif
 template <int MODE, bool IGN, bool X64>
-void launch_pass1(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s) {
+void launch_pass1(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s, const P1Ev &ev) {
 #ifdef KBZ_ABLATION
   // timing-only builds: KBZ_ABL selects the ablation, KBZ_DEPTH the register ring depth
   static const int abl = getenv("KBZ_ABL") ? atoi(getenv("KBZ_ABL")) : 0;
   static const int depth = getenv("KBZ_DEPTH") ? atoi(getenv("KBZ_DEPTH")) : KBZ_PASS1_DEPTH;
   (void)choice;
+  (void)ev;
   if (abl == 1) return launch_abl<MODE, IGN, X64, 1>(depth, a, chunks, s);
   if (abl == 2) return launch_abl<MODE, IGN, X64, 2>(depth, a, chunks, s);
   if (abl == 3) return launch_abl<MODE, IGN, X64, 3>(depth, a, chunks, s);
@@ -2712,14 +2748,13 @@ void launch_pass1(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s
   if (KBZ_PASS1D && MODE == KBZ_MODE_DYNAMORIO && pass1_is_wide(choice, chunks)) {
     constexpr int RING = (IGN && X64) ? 2 : (IGN || X64) ? 3 : KBZ_PASS1D_RING;
     constexpr int NW = KBZ_PASS1D_NX / 3 * 4;
-    hipLaunchKernelGGL((k_pass1d<IGN, X64, KBZ_PASS1D_NX, RING, KBZ_PASS1D_D>), dim3(chunks),
-                       dim3(64 * NW), 0, s, a);
+    p1_launch(k_pass1d<IGN, X64, KBZ_PASS1D_NX, RING, KBZ_PASS1D_D>, dim3(chunks), dim3(64 * NW),
+              s, ev, a);
   } else if (pass1_is_wide(choice, chunks))
-    hipLaunchKernelGGL((k_pass1w<MODE, IGN, X64, kWideNX, kWideNL, kWideD>), dim3(chunks),
-                       dim3(64 * (kWideNL + kWideNX)), 0, s, a);
+    p1_launch(k_pass1w<MODE, IGN, X64, kWideNX, kWideNL, kWideD>, dim3(chunks),
+              dim3(64 * (kWideNL + kWideNX)), s, ev, a);
   else
-    hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, 0, KBZ_PASS1_DEPTH>), dim3(chunks), dim3(128), 0,
-                       s, a);
+    p1_launch(k_pass1s<MODE, IGN, X64, 0, KBZ_PASS1_DEPTH>, dim3(chunks), dim3(128), s, ev, a);
 #endif
 }
 
@@ -2730,43 +2765,43 @@ void launch_pass1(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s
 #define KBZ_PASS1N_WD 2
 #endif
 template <int MODE>
-void launch_pass1n(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s) {
+void launch_pass1n(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s, const P1Ev &ev) {
   if (pass1_is_wide(choice, chunks))
-    hipLaunchKernelGGL((k_pass1n<MODE, 8, KBZ_PASS1N_WD>), dim3(chunks), dim3(512), 0, s, a);
+    p1_launch(k_pass1n<MODE, 8, KBZ_PASS1N_WD>, dim3(chunks), dim3(512), s, ev, a);
   else
-    hipLaunchKernelGGL((k_pass1n<MODE, 2, KBZ_PASS1N_D>), dim3(chunks), dim3(128), 0, s, a);
+    p1_launch(k_pass1n<MODE, 2, KBZ_PASS1N_D>, dim3(chunks), dim3(128), s, ev, a);
 }
 
 // hashed == false: an AFL-mode batch that wants neither hash (k_pass1n)
 int pass1_dispatch(kbz_ctx *c, const Pass1Args &a, uint32_t chunks, bool x64, bool hashed,
-                   hipStream_t s) {
+                   hipStream_t s, const P1Ev &ev) {
   const bool ign = c->ignore != nullptr && c->mode == KBZ_MODE_DYNAMORIO;
   if (!hashed && c->mode == KBZ_MODE_AFL) {
-    launch_pass1n<KBZ_MODE_AFL>(c->pass1, a, chunks, s);
+    launch_pass1n<KBZ_MODE_AFL>(c->pass1, a, chunks, s, ev);
     HIP_TRY(hipGetLastError());
     return 0;
   }
   if (!hashed && c->mode == KBZ_MODE_AFL_CLASSIFY) {
-    launch_pass1n<KBZ_MODE_AFL_CLASSIFY>(c->pass1, a, chunks, s);
+    launch_pass1n<KBZ_MODE_AFL_CLASSIFY>(c->pass1, a, chunks, s, ev);
     HIP_TRY(hipGetLastError());
     return 0;
   }
   switch (c->mode) {
     case KBZ_MODE_AFL:
-      x64 ? launch_pass1<KBZ_MODE_AFL, false, true>(c->pass1, a, chunks, s)
-          : launch_pass1<KBZ_MODE_AFL, false, false>(c->pass1, a, chunks, s);
+      x64 ? launch_pass1<KBZ_MODE_AFL, false, true>(c->pass1, a, chunks, s, ev)
+          : launch_pass1<KBZ_MODE_AFL, false, false>(c->pass1, a, chunks, s, ev);
       break;
     case KBZ_MODE_AFL_CLASSIFY:
-      x64 ? launch_pass1<KBZ_MODE_AFL_CLASSIFY, false, true>(c->pass1, a, chunks, s)
-          : launch_pass1<KBZ_MODE_AFL_CLASSIFY, false, false>(c->pass1, a, chunks, s);
+      x64 ? launch_pass1<KBZ_MODE_AFL_CLASSIFY, false, true>(c->pass1, a, chunks, s, ev)
+          : launch_pass1<KBZ_MODE_AFL_CLASSIFY, false, false>(c->pass1, a, chunks, s, ev);
       break;
     default:
       if (ign)
-        x64 ? launch_pass1<KBZ_MODE_DYNAMORIO, true, true>(c->pass1, a, chunks, s)
-            : launch_pass1<KBZ_MODE_DYNAMORIO, true, false>(c->pass1, a, chunks, s);
+        x64 ? launch_pass1<KBZ_MODE_DYNAMORIO, true, true>(c->pass1, a, chunks, s, ev)
+            : launch_pass1<KBZ_MODE_DYNAMORIO, true, false>(c->pass1, a, chunks, s, ev);
       else
-        x64 ? launch_pass1<KBZ_MODE_DYNAMORIO, false, true>(c->pass1, a, chunks, s)
-            : launch_pass1<KBZ_MODE_DYNAMORIO, false, false>(c->pass1, a, chunks, s);
+        x64 ? launch_pass1<KBZ_MODE_DYNAMORIO, false, true>(c->pass1, a, chunks, s, ev)
+            : launch_pass1<KBZ_MODE_DYNAMORIO, false, false>(c->pass1, a, chunks, s, ev);
   }
   HIP_TRY(hipGetLastError());
   return 0;
@@ -3042,7 +3077,7 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
   a.vcur = c->V[c->vcur];
   a.tflags = c->tflags;
   a.nfw = c->nfw;
-  hipEvent_t *ev = nullptr;
+  P1Ev pev;
   if (c->timing) {
     if (c->ev_used_n == c->ev_pass1.size()) {
       std::pair<hipEvent_t, hipEvent_t> e;
@@ -3052,11 +3087,16 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
       HIP_TRY(hipEventCreateWithFlags(&e.second, KBZ_EVENT_SCOPE));
       c->ev_pass1.push_back(e);
     }
-    ev = &c->ev_pass1[c->ev_used_n++].first;
-    HIP_TRY(hipEventRecord(ev[0], s));
+    pev.start = c->ev_pass1[c->ev_used_n].first;
+    pev.stop = c->ev_pass1[c->ev_used_n++].second;
+#ifdef KBZ_ABLATION  // timing-only builds launch through launch_abl: marker events around it
+    HIP_TRY(hipEventRecord(pev.start, s));
+#endif
   }
-  if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, hashed, s)) return -1;
-  if (ev) HIP_TRY(hipEventRecord(c->ev_pass1[c->ev_used_n - 1].second, s));
+  if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, hashed, s, pev)) return -1;
+#ifdef KBZ_ABLATION
+  if (pev.stop) HIP_TRY(hipEventRecord(pev.stop, s));
+#endif
   if (c->mode == KBZ_MODE_DYNAMORIO) {  // the skip rule for rows j >= 1 needs no other shard
     hipEvent_t st0;
     if (stage_begin(c, s, &st0)) return -1;
