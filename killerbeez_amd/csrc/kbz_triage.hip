@@ -2014,6 +2014,96 @@ __device__ __forceinline__ void emit_items_wave(uint32_t chunk, int k, uint32_t 
   if (staged) st.n += total;
 }
 
+#ifndef KBZ_SCAN_INLINE  // 1: k_scan resolves chunks with few claimed bytes itself (no item, no
+#define KBZ_SCAN_INLINE 1  // append, no k_resolve work); 0: per-byte items for k_resolve
+#endif
+struct ClaimArgs {  // what k_scan needs to resolve claims inline (k_resolve's inputs)
+  const uint8_t *traces;
+  size_t stride;
+  uint32_t n;
+  int mode;
+  const int8_t *outcome;
+  const uint8_t *skip;
+  uint32_t *hnb32;
+  uint32_t *err;
+};
+__device__ __forceinline__ uint32_t pick4(uint4 v, int i) {  // i wave-uniform
+  return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+}
+// Claimed bytes of one wave-window of chunk `chunk`, resolved by this wave: for each claimed byte
+// (up to 8 per round trip) lane r reads that byte of the chunk's row r, and per new bit the first
+// row holding it (class k, not skipped) scores 1, or 2 if the byte was all-virgin and it is the
+// first row with a nonzero byte there -- k_resolve's per-item rule, without the item.
+__device__ void resolve_bytes_inline(const ClaimArgs &ca, uint32_t chunk, int k, uint32_t col,
+                                     uint4 nb, uint4 vir, uint4 prev) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t row = (uint64_t)chunk * kChunk + lane;
+  const uint64_t rc = min(row, (uint64_t)ca.n - 1);
+  const int oc = ca.outcome ? ca.outcome[rc] : KBZ_FUZZ_NONE;
+  const uint8_t sk = ca.skip ? ca.skip[rc] : 0;
+  const int xf = class_xf(ca.mode, k);
+  const uint8_t *rowp = ca.traces + rc * ca.stride;
+  uint32_t rem = 0;  // this lane's claimed bytes, bit i = byte i of its 16
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t w = pick4(nb, i);
+#pragma unroll
+    for (int b = 0; b < 4; b++) rem |= ((w >> (8 * b)) & 0xffu) ? 1u << (4 * i + b) : 0u;
+  }
+  uint64_t lanes = __ballot(rem != 0);
+  while (lanes) {
+    uint32_t cc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nbits[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    bool f2[8] = {false, false, false, false, false, false, false, false};
+    int m = 0;
+    while (lanes && m < 8) {  // wave-uniform scalar work
+      const int L = __builtin_ctzll(lanes);
+      const uint32_t r = __builtin_amdgcn_readlane(rem, L);
+      const int b = __builtin_ctz(r), wi = b >> 2, sh = 8 * (b & 3);
+      nbits[m] = (__builtin_amdgcn_readlane(pick4(nb, wi), L) >> sh) & 0xffu;
+      const uint32_t vb = (__builtin_amdgcn_readlane(pick4(vir, wi), L) >> sh) & 0xffu;
+      const uint32_t pb = (__builtin_amdgcn_readlane(pick4(prev, wi), L) >> sh) & 0xffu;
+      f2[m] = vb == 0xffu && pb == 0;
+      cc[m] = __builtin_amdgcn_readlane(col, L) + b;
+      if (lane == L) rem &= ~(1u << b);
+      if (r == (1u << b)) lanes &= lanes - 1;
+      m++;
+    }
+    uint32_t raw[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) raw[j] = j < m ? rowp[cc[j]] : 0u;  // loads in flight together
+    const bool ok = row < ca.n && class_of(ca.mode, oc) == k && !sk;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if (j >= m) break;
+      const uint32_t tb = ok ? byte_xform(raw[j], xf) : 0u;
+      const uint64_t first_nz = __ballot(tb != 0);
+      uint64_t claimers = 0;
+      for (int bit = 0; bit < 8; bit++) {
+        if ((nbits[j] >> bit) & 1) {
+          const uint64_t mm = __ballot((tb >> bit) & 1);
+          if (!mm && lane == 0) atomicOr(ca.err, 2u);  // k_scan's OR says some row has it
+          claimers |= mm & (0 - mm);
+        }
+      }
+      if ((claimers >> lane) & 1) {
+        const bool two = f2[j] && first_nz && (lane == __builtin_ctzll(first_nz));
+        atomicMax(&ca.hnb32[row], two ? 2u : 1u);
+      }
+    }
+  }
+}
+// number of claimed (nonzero) bytes over the wave: 16 per lane at most, 5 ballots
+__device__ __forceinline__ uint32_t wave_claimed_bytes(uint4 nb) {
+  uint32_t cnt = 0;
+  const uint32_t w[4] = {nb.x, nb.y, nb.z, nb.w};
+#pragma unroll
+  for (int i = 0; i < 4; i++) cnt += __popc(nonzero_bytes8(w[i]) & 0x80808080u);
+  uint32_t total = 0;
+#pragma unroll
+  for (int b = 0; b < 5; b++) total += (uint32_t)__popcll(__ballot((cnt >> b) & 1)) << b;
+  return total;
+}
+
 // Per (segment, 16-B column group): walk the segment's chunks in order with the running OR
 // `prev` (seeded with the OR of earlier segments and earlier shards); bits a chunk adds
 // that are still virgin become claim items.  Blocks of segment 0 also write V' = V & ~total.
@@ -2029,7 +2119,8 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
                                                const uint8_t *ignore, uint64_t *items,
                                                uint32_t cap, uint32_t *counters,
                                                const uint64_t *tflags, uint32_t nfw,
-                                               const uint32_t *listed, uint32_t win_items) {
+                                               const uint32_t *listed, uint32_t win_items,
+                                               ClaimArgs ca) {
   // no per-lane early return: every lane of a wave takes part in the item-allocation prefix
   const uint32_t col0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
   const bool live = col0 < map_size;
@@ -2118,10 +2209,14 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
         if (!st[u]) o[u] = make_uint4(0, 0, 0, 0);  // nothing still virgin in that tile
         const uint4 nb = make_uint4(o[u].x & vr.x & ~prev.x, o[u].y & vr.y & ~prev.y,
                                     o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
-        if (!(KBZ_SCAN_ABL & 1) && __ballot(nb.x | nb.y | nb.z | nb.w))  // wave-uniform
-          emit_items_wave(c, k, col, nb, vir, prev, stg, items, cap, counters,
-                          (uint8_t *)chunk_or + (size_t)c * nclass * map_size + kc, live,
-                          win_items);
+        if (!(KBZ_SCAN_ABL & 1) && __ballot(nb.x | nb.y | nb.z | nb.w)) {  // wave-uniform
+          if (KBZ_SCAN_INLINE && wave_claimed_bytes(nb) < win_items)
+            resolve_bytes_inline(ca, c, k, col, nb, vir, prev);
+          else
+            emit_items_wave(c, k, col, nb, vir, prev, stg, items, cap, counters,
+                            (uint8_t *)chunk_or + (size_t)c * nclass * map_size + kc, live,
+                            win_items);
+        }
         prev = or4(prev, o[u]);
       }
     }
@@ -3257,7 +3352,10 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
                      c->cur_chunks, c->cur_seg_len, c->nc, (uint32_t)c->M, c->segprev, nseg,
                      c->total, prefix, total, c->V[c->vcur], c->V[vn], ign, c->items,
                      c->item_cap, c->counters, c->tflags, c->nfw,
-                     c->mode == KBZ_MODE_DYNAMORIO ? c->flags : nullptr, c->win_items);
+                     c->mode == KBZ_MODE_DYNAMORIO ? c->flags : nullptr, c->win_items,
+                     ClaimArgs{c->cur_traces, c->cur_stride, (uint32_t)c->cur_n, c->mode,
+                               c->cur_outcome, c->mode == KBZ_MODE_DYNAMORIO ? c->skip : nullptr,
+                               c->hnb32, c->counters + 2});
   HIP_TRY(hipGetLastError());
   if (stage_end(c, s, KBZ_STAGE_SCAN, st0)) return -1;
   if (c->cur_n) {

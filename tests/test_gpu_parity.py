@@ -726,7 +726,8 @@ def test_claim_overflow_is_reported_once(gpu, monkeypatch):
     from killerbeez_amd import plugin as P
 
     monkeypatch.setenv("KBZ_DEBUG_ITEM_CAP", "16")
-    m = 4096
+    monkeypatch.setenv("KBZ_DEBUG_WIN_ITEMS", "1")  # every claimed window an item (k_scan would
+    m = 4096                                         # resolve windows of few claims itself)
     t, oc = synth.sparse_np(300, m, seed=2529, hot_frac=0.05)
     p = P.Plugin("afl_gpu", '{"map_size": %d, "max_batch": 256}' % m)
     with pytest.raises(RuntimeError, match="overflow"):
