@@ -747,9 +747,10 @@ def test_claim_overflow_is_reported_once(gpu, monkeypatch):
 @pytest.mark.parametrize("win", ["1", "16", "1000000"], ids=["all-windows", "default", "no-windows"])
 @pytest.mark.parametrize("mode", MODES)
 def test_claims_window_and_byte_items(gpu, mode, win, monkeypatch):
-    """The two claim paths of k_resolve give identical results: per-byte items (one scattered
-    byte of each of the chunk's rows) and window items (the chunk's 1-KiB column window streamed
-    row by row in order).  Fresh virgin maps and dense rows make windows with hundreds of
+    """The claim paths give identical results: k_scan resolving a window's few claimed bytes
+    itself (one byte of each of the chunk's rows per claim, 8 claims per round trip; the
+    per-byte items of KBZ_SCAN_INLINE=0 builds follow the same rule in k_resolve) and window
+    items (k_resolve streams the chunk's 1-KiB column window row by row in order).  Fresh virgin maps and dense rows make windows with hundreds of
     claimed bytes, sparse rows windows with one or two; a 4,864-B map leaves lanes of its last window
     past the end; partial last chunk; DynamoRIO with ignore bytes and repeated execs (skipped
     rows must not claim), AFL with hangs/crashes (simplified classes: every byte claims)."""
