@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
+#include <utility>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstdio>
@@ -50,6 +52,14 @@ template <int V>
 struct IntC {  // a compile-time int passed to generic lambdas
   static constexpr int value = V;
 };
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F &f, std::integer_sequence<int, I...>) {
+  (f(IntC<I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {  // f(IntC<0>{}), ..., f(IntC<N - 1>{})
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 __host__ __device__ __forceinline__ int mode_nclass(int mode) {
   return mode == KBZ_MODE_DYNAMORIO ? 1 : 3;
@@ -1331,9 +1341,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
                         // 2 = N only hands slots back, 4 = X skips classify, 8 = X skips the mix
 #define KBZ_PASS1D_ABL 0
 #endif
-#ifndef KBZ_PASS1D_SPEC  // 1: C reads tile t + 1's words inside chain(t) (see step)
-#define KBZ_PASS1D_SPEC 1
-#endif
 #ifndef KBZ_PASS1D_CN  // 1: without ignore bytes C runs the neighbour test itself, in its chain's
 #define KBZ_PASS1D_CN 0   // dependency bubbles (wave 4 idles with NX = 6, is an X wave with NX = 7)
 #endif
@@ -1381,25 +1388,24 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
     uint64_t h = (uint64_t)(kHashConst ^ a.map_size);
     uint64_t x0 = kXP1 + kXP2, x1 = kXP2, x2 = 0, x3 = 0 - kXP1;
     uint4 kb[2][SLOTS];  // tile t's k words in kb[t & 1], read one tile ahead
-    auto read_k = [&](uint32_t t, auto bc) {
-      constexpr int b = decltype(bc)::value;
-      const int sl = (int)(t % RING);
+    // Slots are compile-time constants (the tile loop is unrolled by the ring size, and by twice
+    // that for an odd ring so the kb parity repeats): every LDS address is a loop-invariant
+    // register plus an immediate offset, no address arithmetic per read.
+    auto read_k = [&](auto bc, auto sc) {  // the words of the tile in slot sc into kb[bc]
+      constexpr int b = decltype(bc)::value, sl = decltype(sc)::value;
 #pragma unroll
       for (int q = 0; q < SLOTS; q++) kb[b][q] = kring[sl * TILE + lane * SLOTS + (q ^ sw)];
     };
     uint32_t nacc_lo = 0, nacc_hi = 0;  // CN: OR over the row's words of (word ^ previous row's)
-    // SPEC: chain(t) also reads tile t + 1's words, one ds_read_b128 per two steps (they issue
-    // in the chain's dependency gaps instead of as a burst of 16 between two tiles)
-    auto chain = [&](uint32_t t, auto bc) {
-      constexpr int b = decltype(bc)::value;
-      const int sl1 = (int)((t + 1) % RING);
+    // chain the tile in kb[b] (slot sl); tile t + 1's words (slot sl + 1) are read meanwhile, one
+    // ds_read_b128 per two steps (in the chain's dependency gaps, not as a burst of 16)
+    auto chain = [&](auto bc, auto sc) {
+      constexpr int b = decltype(bc)::value, sl = decltype(sc)::value, sl1 = (sl + 1) % RING;
       if (!(KBZ_PASS1D_ABL & 1)) {
 #pragma unroll
         for (int q = 0; q < SLOTS; q++) {
-          if (KBZ_PASS1D_SPEC) {
-            kb[b ^ 1][q] = kring[sl1 * TILE + lane * SLOTS + (q ^ sw)];
-            __builtin_amdgcn_sched_barrier(0);
-          }
+          kb[b ^ 1][q] = kring[sl1 * TILE + lane * SLOTS + (q ^ sw)];
+          __builtin_amdgcn_sched_barrier(0);
           const uint4 kq = kb[b][q];
           h = h32_step_fast(h, (uint64_t)kq.x | ((uint64_t)kq.y << 32));
           h = h32_step_fast(h, (uint64_t)kq.z | ((uint64_t)kq.w << 32));
@@ -1416,7 +1422,6 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
         for (int q = 0; q < SLOTS; q++) h ^= kb[b][q].x;
       }
       if (X64) {
-        const int sl = (int)(t % RING);
 #pragma unroll 4
         for (int q = 0; q < SLOTS; q++) {
           const uint4 v = tring[sl * TILE + lane * SLOTS + (q ^ sw)];
@@ -1432,68 +1437,44 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
         }
       }
     };
-    // tile t: its words came in with the previous step; read t + 1's, chain t, then free t
-    // (XXH64 reads its own ring in the chain step, so the slot is freed after it)
     KBZ_STAMP_DECL;
-#if KBZ_PASS1D_SPEC
-    // The flag of tile t + 1's slot is read before the chain's speculative reads of its words:
-    // a wave's LDS operations execute in order, so if the flag says "ready", the words are tile
-    // t + 1's.  Otherwise they are read again once it does.  Slot t + 1 is freed (without XXH64)
-    // when its words are in registers: at the end of step t.
-    auto step = [&](uint32_t t, auto bc) {
-      constexpr int b = decltype(bc)::value;
+    // Step t (in slot sl, words in kb[b]): the flag of slot sl + 1 is read before the chain's
+    // speculative reads of its words: a wave's LDS operations execute in order, so if the flag
+    // says "ready", the words are tile t + 1's.  Otherwise they are read again once it does.
+    // Slot sl + 1 is freed (without XXH64) when its words are in registers: at the end of step t;
+    // with XXH64 slot sl is, after the chain read its classified words.
+    auto step = [&](uint32_t t, auto bc, auto sc) {
+      constexpr int b = decltype(bc)::value, sl = decltype(sc)::value, sl1 = (sl + 1) % RING;
       const bool more = t + 1 < ntiles;
-      const int f = KBZ_FLD(ready, (t + 1) % RING);
+      const int f = KBZ_FLD(ready, sl1);
       asm volatile("" ::: "memory");  // the flag read stays ahead of the word reads
       KBZ_STAMP(3);
-      chain(t, bc);
+      chain(bc, sc);
       KBZ_STAMP(0);
       if (more && f != (int)(t + 1)) {
         wait_ready(t + 1);
         KBZ_STAMP(1);
-        read_k(t + 1, IntC<b ^ 1>{});
+        read_k(IntC<b ^ 1>{}, IntC<sl1>{});
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile t + 1's words have arrived
       KBZ_STAMP(2);
       if (lane == 0) {
-        if (X64) KBZ_FST(freed_c, t % RING, (int)t);
-        else if (more) KBZ_FST(freed_c, (t + 1) % RING, (int)(t + 1));
+        if (X64) KBZ_FST(freed_c, sl, (int)t);
+        else if (more) KBZ_FST(freed_c, sl1, (int)(t + 1));
       }
     };
-#else
-    auto step = [&](uint32_t t, auto bc) {
-      constexpr int b = decltype(bc)::value;
-      // tile t + 1 already written: its reads overlap this chain; else they follow it
-      const bool more = t + 1 < ntiles;
-      const bool pre = more && KBZ_FLD(ready, (t + 1) % RING) == (int)(t + 1);
-      asm volatile("" ::: "memory");
-      if (pre) read_k(t + 1, IntC<b ^ 1>{});
-      if (!X64 && lane == 0) KBZ_FST(freed_c, t % RING, (int)t);  // slot t's words are in registers
-      KBZ_STAMP(3);
-      chain(t, bc);
-      KBZ_STAMP(0);
-      if (more && !pre) {
-        wait_ready(t + 1);
-        KBZ_STAMP(1);
-        read_k(t + 1, IntC<b ^ 1>{});
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile t + 1's words have arrived
-      KBZ_STAMP(2);
-      if (X64 && lane == 0) KBZ_FST(freed_c, t % RING, (int)t);
-    };
-#endif
     if (ntiles) {
       wait_ready(0);
-      read_k(0, IntC<0>{});
+      read_k(IntC<0>{}, IntC<0>{});
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (KBZ_PASS1D_SPEC && !X64 && lane == 0) KBZ_FST(freed_c, 0, 0);
+      if (!X64 && lane == 0) KBZ_FST(freed_c, 0, 0);
     }
-    uint32_t t = 0;
-    for (; t + 1 < ntiles; t += 2) {
-      step(t, IntC<0>{});
-      step(t + 1, IntC<1>{});
-    }
-    if (t < ntiles) step(t, IntC<0>{});
+    constexpr int U = (RING % 2 == 0) ? RING : 2 * RING;
+    for (uint32_t t0 = 0; t0 < ntiles; t0 += U)
+      static_for<U>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        if (t0 + u < ntiles) step(t0 + u, IntC<u & 1>{}, IntC<u % RING>{});
+      });
     KBZ_STAMP_FLUSH(chunk * 16 + wave);
     if (lane < nrows) {
       const uint32_t h32 = h32_final(h);
@@ -1521,12 +1502,15 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
 #endif
     uint64_t nacc = 0;  // OR over the row's words of (word ^ previous row's word)
     const uint4 *ring = IGN ? wring : kring;
-    for (uint32_t t = 0; t < ntiles; t++) {
+    for (uint32_t t0 = 0; t0 < ntiles; t0 += RING)
+      static_for<RING>([&](auto sc) {  // slots as compile-time constants (see C)
+      constexpr int sl = decltype(sc)::value;
+      const uint32_t t = t0 + sl;
+      if (t >= ntiles) return;
       wait_ready(t);
-      const int sl = (int)(t % RING);
       if (KBZ_PASS1D_ABL & 2) {
         if (lane == 0) KBZ_FST(freed_n, sl, (int)t);
-        continue;
+        return;
       }
       uint4 vv[SLOTS];
 #pragma unroll
@@ -1539,7 +1523,7 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
         const uint64_t w1 = (uint64_t)vv[q].z | ((uint64_t)vv[q].w << 32);
         nacc |= (w0 ^ from_prev_lane(w0)) | (w1 ^ from_prev_lane(w1));
       }
-    }
+    });
     // lane 0 has no predecessor in the wave: a placeholder (k_skip compares chunk starts)
     if (lane < nrows) a.neq[row0 + lane] = nacc != 0;
   } else if ((wave & 3) == 0) {
