@@ -592,8 +592,10 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
       }
       uint4 *row = &lds[b * TILE + lane * SLOTS];
       const int sw = lane & 15;
-      constexpr int TP = KBZ_PASS1_TPRE;  // slots in flight: a mostly-zero slot takes a few
-      uint4 vring[TP];                    // instructions, far less than an LDS round trip
+      // slots in flight: a mostly-zero slot takes a few instructions, far less than an LDS round
+      // trip (deeper register rings, timing-only builds, keep 2: their VGPRs are spent)
+      constexpr int TP = D > 2 ? 2 : KBZ_PASS1_TPRE;
+      uint4 vring[TP];
 #pragma unroll
       for (int j = 0; j < TP; j++) vring[j] = row[j ^ sw];
 #pragma unroll 1
