@@ -187,6 +187,14 @@ __device__ __forceinline__ void vmcnt_wait_ring(u32x4 (&r)[9]) {
                : "n"(N)
                : "memory");
 }
+// The same with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane offset (the saddr
+// form): moving the base costs SALU only, no 64-bit VALU address add per load.
+__device__ __forceinline__ void asm_load16_s(u32x4 &r, uint32_t voff, const uint8_t *sbase) {
+  asm volatile("global_load_dwordx4 %0, %1, %2 nt" : "=v"(r) : "v"(voff), "s"(sbase) : "memory");
+}
+__device__ __forceinline__ void asm_load16_s_cached(u32x4 &r, uint32_t voff, const uint8_t *sbase) {
+  asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(r) : "v"(voff), "s"(sbase) : "memory");
+}
 // cached (not nontemporal) 16-B load: data every workgroup re-reads (the virgin maps)
 __device__ __forceinline__ void asm_load16_cached(u32x4 &r, const uint8_t *p) {
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
@@ -1537,25 +1545,26 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
     if (wave >= 4) __builtin_amdgcn_s_setprio(KBZ_PASS1D_XPRIO);
 #endif
     const int lr = lane / SLOTS, ls = lane % SLOTS;
-    const uint8_t *lbase = a.traces + row0 * a.stride + ls * 16;
+    const uint8_t *cbase = a.traces + row0 * a.stride;  // the chunk's rows: < 64 x 32 MiB
     const uint32_t rstep = (uint32_t)(RPI * a.stride);
     const uint32_t rlast = (uint32_t)((nrows - 1) * a.stride);
-    const uint8_t *vbase = a.vcur + (size_t)ls * 16;
-    const uint8_t *gbase = IGN ? a.ignore + (size_t)ls * 16 : nullptr;
+    uint32_t voff[NLD];  // per lane: its row of each load and its 16-B slot (loop-invariant)
+#pragma unroll
+    for (int i = 0; i < NLD; i++)
+      voff[i] = min((uint32_t)(i * rstep + lr * a.stride), rlast) + (uint32_t)ls * 16;
+    const uint32_t vsl = (uint32_t)ls * 16;
     const uint32_t nmine = ntiles > (uint32_t)xi ? (ntiles - 1 - xi) / NX + 1 : 0;
     const uint32_t nb = (nmine + D - 1) / D * D;
     auto tile_of = [&](uint32_t q) { return (uint32_t)xi + q * NX; };
-    // branch-free asm loads (see k_pass1s); steps past the wave's last tile re-load its first
+    // branch-free asm loads (see k_pass1s); steps past the wave's last tile re-load its first.
+    // The tile's offset moves the SGPR base (saddr form), the lanes' offsets stay put.
     auto load = [&](u32x4 (&r)[NR], uint32_t q) {
       const uint32_t t = q < nmine ? tile_of(q) : (uint32_t)xi;
       const uint32_t tt = t < ntiles ? t : 0;
 #pragma unroll
-      for (int i = 0; i < NLD; i++) {
-        const uint32_t off = min((uint32_t)(i * rstep + lr * a.stride), rlast);
-        asm_load16(r[i], lbase + (size_t)tt * TW + off);
-      }
-      asm_load16_cached(r[NLD], vbase + (size_t)tt * TW);
-      if (IGN) asm_load16_cached(r[NLD + 1], gbase + (size_t)tt * TW);
+      for (int i = 0; i < NLD; i++) asm_load16_s(r[i], voff[i], cbase + (size_t)tt * TW);
+      asm_load16_s_cached(r[NLD], vsl, a.vcur + (size_t)tt * TW);
+      if (IGN) asm_load16_s_cached(r[NLD + 1], vsl, a.ignore + (size_t)tt * TW);
     };
     u32x4 R[D][NR];
 #pragma unroll
