@@ -2025,19 +2025,63 @@ struct ClaimArgs {  // what k_scan needs to resolve claims inline (k_resolve's i
 __device__ __forceinline__ uint32_t pick4(uint4 v, int i) {  // i wave-uniform
   return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
 }
-// Claimed bytes of one wave-window of chunk `chunk`, resolved by this wave: for each claimed byte
-// (up to 8 per round trip) lane r reads that byte of the chunk's row r, and per new bit the first
-// row holding it (class k, not skipped) scores 1, or 2 if the byte was all-virgin and it is the
-// first row with a nonzero byte there -- k_resolve's per-item rule, without the item.
-__device__ void resolve_bytes_inline(const ClaimArgs &ca, uint32_t chunk, int k, uint32_t col,
-                                     uint4 nb, uint4 vir, uint4 prev) {
+// Claimed bytes resolved by k_scan's wave itself.  They are queued (per wave, in LDS: chunk,
+// byte column, new bits, the "2" candidate flag) over the chunks of the walk and resolved 8 at
+// a time, all 8 rows' bytes (and their chunk's outcome / skip flags) in flight together: lane r
+// reads the byte of row r of the claim's chunk, and per new bit the first row holding it
+// (class k, not skipped) scores 1, or 2 if the byte was all-virgin and it is the first row with
+// a nonzero byte there -- k_resolve's per-item rule, without the item.
+constexpr int kClaimQ = 8;
+struct ClaimQ {
+  uint4 *q;  // this wave's kClaimQ entries in LDS: {chunk, column, new bits | f2 << 8, 0}
+  int m;     // wave-uniform fill
+};
+__device__ void claims_flush(const ClaimArgs &ca, int k, ClaimQ &cq) {
+  if (!cq.m) return;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // lane 0's entries are written
   const int lane = threadIdx.x & 63;
-  const uint64_t row = (uint64_t)chunk * kChunk + lane;
-  const uint64_t rc = min(row, (uint64_t)ca.n - 1);
-  const int oc = ca.outcome ? ca.outcome[rc] : KBZ_FUZZ_NONE;
-  const uint8_t sk = ca.skip ? ca.skip[rc] : 0;
   const int xf = class_xf(ca.mode, k);
-  const uint8_t *rowp = ca.traces + rc * ca.stride;
+  uint4 e[kClaimQ];
+  uint32_t raw[kClaimQ];
+  int oc[kClaimQ];
+  uint8_t sk[kClaimQ];
+#pragma unroll
+  for (int j = 0; j < kClaimQ; j++) e[j] = j < cq.m ? cq.q[j] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < kClaimQ; j++) {  // loads in flight together
+    const uint64_t rc = min((uint64_t)e[j].x * kChunk + lane, (uint64_t)ca.n - 1);
+    raw[j] = j < cq.m ? ca.traces[rc * ca.stride + e[j].y] : 0u;
+    oc[j] = (j < cq.m && ca.outcome) ? ca.outcome[rc] : KBZ_FUZZ_NONE;
+    sk[j] = (j < cq.m && ca.skip) ? ca.skip[rc] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < kClaimQ; j++) {
+    if (j >= cq.m) break;  // wave-uniform
+    const uint64_t row = (uint64_t)e[j].x * kChunk + lane;
+    const bool ok = row < ca.n && class_of(ca.mode, oc[j]) == k && !sk[j];
+    const uint32_t nbits = e[j].z & 0xffu;
+    const uint32_t tb = ok ? byte_xform(raw[j], xf) : 0u;
+    const uint64_t first_nz = __ballot(tb != 0);
+    uint64_t claimers = 0;
+    for (int bit = 0; bit < 8; bit++) {
+      if ((nbits >> bit) & 1) {
+        const uint64_t mm = __ballot((tb >> bit) & 1);
+        if (!mm && lane == 0) atomicOr(ca.err, 2u);  // k_scan's OR says some row has it
+        claimers |= mm & (0 - mm);
+      }
+    }
+    if ((claimers >> lane) & 1) {
+      const bool two = (e[j].z >> 8) && first_nz && (lane == __builtin_ctzll(first_nz));
+      atomicMax(&ca.hnb32[row], two ? 2u : 1u);
+    }
+  }
+  asm volatile("" ::: "memory");
+  cq.m = 0;
+}
+// Queue the claimed bytes of this wave's window of chunk `chunk` (flushing every kClaimQ).
+__device__ void claims_enqueue(const ClaimArgs &ca, int k, ClaimQ &cq, uint32_t chunk,
+                               uint32_t col, uint4 nb, uint4 vir, uint4 prev) {
+  const int lane = threadIdx.x & 63;
   uint32_t rem = 0;  // this lane's claimed bytes, bit i = byte i of its 16
 #pragma unroll
   for (int i = 0; i < 4; i++) {
@@ -2046,45 +2090,19 @@ __device__ void resolve_bytes_inline(const ClaimArgs &ca, uint32_t chunk, int k,
     for (int b = 0; b < 4; b++) rem |= ((w >> (8 * b)) & 0xffu) ? 1u << (4 * i + b) : 0u;
   }
   uint64_t lanes = __ballot(rem != 0);
-  while (lanes) {
-    uint32_t cc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nbits[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    bool f2[8] = {false, false, false, false, false, false, false, false};
-    int m = 0;
-    while (lanes && m < 8) {  // wave-uniform scalar work
-      const int L = __builtin_ctzll(lanes);
-      const uint32_t r = __builtin_amdgcn_readlane(rem, L);
-      const int b = __builtin_ctz(r), wi = b >> 2, sh = 8 * (b & 3);
-      nbits[m] = (__builtin_amdgcn_readlane(pick4(nb, wi), L) >> sh) & 0xffu;
-      const uint32_t vb = (__builtin_amdgcn_readlane(pick4(vir, wi), L) >> sh) & 0xffu;
-      const uint32_t pb = (__builtin_amdgcn_readlane(pick4(prev, wi), L) >> sh) & 0xffu;
-      f2[m] = vb == 0xffu && pb == 0;
-      cc[m] = __builtin_amdgcn_readlane(col, L) + b;
-      if (lane == L) rem &= ~(1u << b);
-      if (r == (1u << b)) lanes &= lanes - 1;
-      m++;
-    }
-    uint32_t raw[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) raw[j] = j < m ? rowp[cc[j]] : 0u;  // loads in flight together
-    const bool ok = row < ca.n && class_of(ca.mode, oc) == k && !sk;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      if (j >= m) break;
-      const uint32_t tb = ok ? byte_xform(raw[j], xf) : 0u;
-      const uint64_t first_nz = __ballot(tb != 0);
-      uint64_t claimers = 0;
-      for (int bit = 0; bit < 8; bit++) {
-        if ((nbits[j] >> bit) & 1) {
-          const uint64_t mm = __ballot((tb >> bit) & 1);
-          if (!mm && lane == 0) atomicOr(ca.err, 2u);  // k_scan's OR says some row has it
-          claimers |= mm & (0 - mm);
-        }
-      }
-      if ((claimers >> lane) & 1) {
-        const bool two = f2[j] && first_nz && (lane == __builtin_ctzll(first_nz));
-        atomicMax(&ca.hnb32[row], two ? 2u : 1u);
-      }
-    }
+  while (lanes) {  // wave-uniform scalar work
+    const int L = __builtin_ctzll(lanes);
+    const uint32_t r = __builtin_amdgcn_readlane(rem, L);
+    const int b = __builtin_ctz(r), wi = b >> 2, sh = 8 * (b & 3);
+    const uint32_t nbits = (__builtin_amdgcn_readlane(pick4(nb, wi), L) >> sh) & 0xffu;
+    const uint32_t vb = (__builtin_amdgcn_readlane(pick4(vir, wi), L) >> sh) & 0xffu;
+    const uint32_t pb = (__builtin_amdgcn_readlane(pick4(prev, wi), L) >> sh) & 0xffu;
+    const uint32_t cc = __builtin_amdgcn_readlane(col, L) + b;
+    if (lane == 0) cq.q[cq.m] = make_uint4(chunk, cc, nbits | ((vb == 0xffu && pb == 0) ? 0x100u : 0u), 0);
+    cq.m++;
+    if (lane == L) rem &= ~(1u << b);
+    if (r == (1u << b)) lanes &= lanes - 1;
+    if (cq.m == kClaimQ) claims_flush(ca, k, cq);
   }
 }
 // number of claimed (nonzero) bytes over the wave: 16 per lane at most, 5 ballots
@@ -2164,6 +2182,8 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
                         : make_uint4(0, 0, 0, 0);
   __shared__ uint64_t stage_buf[4][kWaveItems];  // 256 threads = 4 waves
   ItemStage stg{stage_buf[threadIdx.x >> 6], 0u};
+  __shared__ uint4 claim_q[4][kClaimQ];
+  ClaimQ cq{claim_q[threadIdx.x >> 6], 0};
   const uint32_t seg_new = (send.x & vr.x & ~prev.x) | (send.y & vr.y & ~prev.y) |
                            (send.z & vr.z & ~prev.z) | (send.w & vr.w & ~prev.w);
   if (!__ballot(seg_new != 0)) return;  // wave-uniform: nothing new in this segment
@@ -2206,7 +2226,7 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
                                     o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
         if (!(KBZ_SCAN_ABL & 1) && __ballot(nb.x | nb.y | nb.z | nb.w)) {  // wave-uniform
           if (KBZ_SCAN_INLINE && wave_claimed_bytes(nb) < win_items)
-            resolve_bytes_inline(ca, c, k, col, nb, vir, prev);
+            claims_enqueue(ca, k, cq, c, col, nb, vir, prev);
           else
             emit_items_wave(c, k, col, nb, vir, prev, stg, items, cap, counters,
                             (uint8_t *)chunk_or + (size_t)c * nclass * map_size + kc, live,
@@ -2216,6 +2236,7 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
       }
     }
   }
+  claims_flush(ca, k, cq);
   flush_items(stg, items, cap, counters);
 }
 
