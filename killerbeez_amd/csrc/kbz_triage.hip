@@ -290,6 +290,9 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #ifndef KBZ_PASS1_LMIX4  // k_pass1s wave L: mixes of 4 words at once, ahead of their chain steps
 #define KBZ_PASS1_LMIX4 0  // 1: 0.83 vs 0.80 ms (VALU), profiles/r03_v10
 #endif
+#ifndef KBZ_PASS1_LPRE  // k_pass1s wave L: iterations (2 LDS slots each) read ahead (1 or 2)
+#define KBZ_PASS1_LPRE 1
+#endif
 #ifndef KBZ_PASS1_TPRE  // k_pass1s wave T: LDS slots read this many slots ahead (1 or 4)
 #define KBZ_PASS1_TPRE 8  // 1 / 4 / 8: 0.80 / 0.767 / 0.744 ms, profiles/r03_v10
 #endif
@@ -418,10 +421,12 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
       const uint4 *row = &lds[b * TILE + lane * SLOTS];
       const int sw = lane & 15;
       uint4 v0 = row[0 ^ sw], v1 = row[1 ^ sw];
-#pragma unroll 1
+      constexpr int LP = KBZ_PASS1_LPRE;  // iterations (of 2 slots) read ahead
+      uint4 u0 = LP > 1 ? row[2 ^ sw] : v0, u1 = LP > 1 ? row[3 ^ sw] : v1;
+#pragma unroll LP
       for (int q = 0; q < SLOTS; q += 2) {
-        // software pipeline: the next two slots are in flight while these 4 words chain
-        const int qn = (q + 2) & (SLOTS - 1);
+        // software pipeline: the next LP x 2 slots are in flight while these 4 words chain
+        const int qn = (q + 2 * LP) & (SLOTS - 1);
         const uint4 n0 = row[qn ^ sw], n1 = row[(qn + 1) ^ sw];
         if (KBZ_PASS1_LMIX4 && !TMIX) {
           // the 4 words' mixes are independent of the chain: computed together, ahead of the 4
@@ -452,8 +457,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
               else x3 = xx_round(x3, tv[j]);
             }
           }
-          v0 = n0;
-          v1 = n1;
+          if (LP > 1) { v0 = u0; v1 = u1; u0 = n0; u1 = n1; } else { v0 = n0; v1 = n1; }
           continue;
         }
 #pragma unroll
@@ -484,8 +488,15 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
             }
           }
         }
-        v0 = n0;
-        v1 = n1;
+        if (LP > 1) {
+          v0 = u0;
+          v1 = u1;
+          u0 = n0;
+          u1 = n1;
+        } else {
+          v0 = n0;
+          v1 = n1;
+        }
       }
     };
     // prologue: own half of tile 0 -> buffer 0 (T transforms it at step 0)
