@@ -296,8 +296,8 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #ifndef KBZ_PASS1_TPRE  // k_pass1s wave T: LDS slots read this many slots ahead (1 or 4)
 #define KBZ_PASS1_TPRE 8  // 1 / 4 / 8: 0.80 / 0.767 / 0.744 ms, profiles/r03_v10
 #endif
-#ifndef KBZ_PASS1_TMIX  // timing variants: 0 = wave L mixes in every mode
-#define KBZ_PASS1_TMIX 1
+#ifndef KBZ_PASS1_TMIX  // which modes' mix wave T computes (see k_pass1s); 0 = none
+#define KBZ_PASS1_TMIX 3
 #endif
 #ifndef KBZ_WIDE_PEEL  // k_pass1w transform waves: steady steps without bounds tests
 #define KBZ_WIDE_PEEL 1
@@ -356,8 +356,12 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   // LDS for wave L (T only simplifies the few hang/crash rows there, L was the slower wave:
   // pass 1 1.23 -> 1.13 ms, profiles/r02_v18).  DynamoRIO and AFL_CLASSIFY keep the mix on L:
   // T's classify makes T the busier wave there.  XXH64 needs the transformed words on L.
-  // KBZ_PASS1_TMIX == 2: T mixes in every mode (then wave L is a bare chain).
-  constexpr bool TMIX = KBZ_PASS1_TMIX == 2 ? !X64 : (KBZ_PASS1_TMIX && MODE == KBZ_MODE_AFL && !X64);
+  // KBZ_PASS1_TMIX: 1 = AFL only, 2 = every mode, 3 (default) = AFL and DynamoRIO.  With T
+  // mixing, wave L is a bare chain: DynamoRIO config 2 pass 1 -2 % same-box since wave T reads
+  // its slots 8 ahead (profiles/r03_v13); AFL_CLASSIFY stays on L (+3 % with T mixing).
+  constexpr bool TMIX = !X64 && (KBZ_PASS1_TMIX == 2 ||
+                                 (KBZ_PASS1_TMIX >= 1 && MODE == KBZ_MODE_AFL) ||
+                                 (KBZ_PASS1_TMIX == 3 && MODE == KBZ_MODE_DYNAMORIO));
   // AFL modes: the simplified classes' column ORs come from their rows, once per tile
   constexpr bool SROWS = KBZ_PASS1_SROWS && NC > 1;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = 8;  // 8 x 1-KiB loads per wave per tile
