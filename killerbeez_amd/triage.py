@@ -63,7 +63,9 @@ class TriageContext:
         check(lib().kbz_ctx_set_pass1(self._h, int(choice)), "kbz_ctx_set_pass1")
 
     def stats(self) -> dict:
-        """Work counters of the last finished batch (kbz_ctx_stats)."""
+        """Work counters of the last finished batch (kbz_ctx_stats).  "claims" counts the claim
+        items appended for k_resolve (window items); claimed bytes k_scan resolves itself are not
+        in it."""
         out = np.zeros(3, np.uint32)
         check(lib().kbz_ctx_stats(self._h, _np_ptr(out)), "kbz_ctx_stats")
         return {"claims": int(out[0]), "fixed_chunks": int(out[1]), "bad_rows": int(out[2])}
