@@ -77,6 +77,10 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch);
 void kbz_ctx_destroy(kbz_ctx_t *ctx);
 const char *kbz_last_error(void);
 int kbz_abi_version(void);
+/* The preprocessor flags this library was built with: "" for the product library that
+ * killerbeez_amd/build.py builds; experiment builds (build_variants/<name>/, timing A/Bs and
+ * diagnostics, never for results) report their -D flags. */
+const char *kbz_build_flags(void);
 
 /* ignore_bytes for KBZ_MODE_DYNAMORIO (dynamorio_instrumentation.c:788-814): map_size bytes of
  * host memory, or NULL to clear.  Same conventions as the reference: hash32_with_ignore ANDs
@@ -227,6 +231,26 @@ int kbz_merge_and_host(uint8_t *out, const uint8_t *states, size_t n, size_t sta
 typedef int (*kbz_merge_fill_fn)(void *user, uint8_t *dst, size_t first, size_t count);
 int kbz_merge_and_fill(uint8_t *out, size_t n, size_t state_bytes, kbz_merge_fill_fn fill,
                        void *user);
+/* The same fold with the result left in device memory d_out (state_bytes, the current device);
+ * ordered after the work queued on `stream` so far, complete when the call returns. */
+int kbz_merge_and_fill_device(uint8_t *d_out, size_t n, size_t state_bytes, kbz_merge_fill_fn fill,
+                              void *user, void *stream);
+/* The merger fold over several GPUs of one node (BASELINE config 4: merger/merger.c:79-104 with
+ * the states sharded across the node's GPUs).  Worker w of ndev (device devices[w]; NULL = every
+ * visible device, one worker each) folds the contiguous share [n*w/ndev, n*(w+1)/ndev) of the
+ * states on its own host thread: fill(user, dst, first, count) is called with global indices,
+ * concurrently from the workers for disjoint ranges (it must be thread-safe).  The partial folds
+ * are then exchanged -- RCCL has no bitwise-AND reduction, so an all-gather over the workers'
+ * GPUs (ncclCommInitAll + ncclAllGather, librccl loaded at run time) followed by a local AND on
+ * every device, or peer / device-local copies of every partial to worker 0's device and one AND
+ * there -- and the merged state is copied to host `out`.  exchange: KBZ_EXCHANGE_AUTO (RCCL when
+ * the devices are distinct and more than one, else copies), KBZ_EXCHANGE_COPY, KBZ_EXCHANGE_RCCL
+ * (fails if RCCL cannot be used).  A device may be listed several times (several workers on one
+ * GPU: the copy path).  *used_out (or NULL) gets the exchange actually used.  Synchronous. */
+enum kbz_exchange { KBZ_EXCHANGE_AUTO = 0, KBZ_EXCHANGE_COPY = 1, KBZ_EXCHANGE_RCCL = 2 };
+int kbz_merge_and_fill_devices(uint8_t *out, size_t n, size_t state_bytes, kbz_merge_fill_fn fill,
+                               void *user, const int *devices, size_t ndev, int exchange,
+                               int *used_out);
 
 /* ---- DynamoRIO per-module coverage ----------------------------------------------------------- */
 /* has_new_coverage_per_module (dynamorio_instrumentation.c:1477-1493) over an ordered batch: each

@@ -19,6 +19,7 @@ _vp, _sz, _i, _u32, _u64 = C.c_void_p, C.c_size_t, C.c_int, C.c_uint32, C.c_uint
 SIGNATURES = [
     ("kbz_abi_version", _i, []),
     ("kbz_last_error", C.c_char_p, []),
+    ("kbz_build_flags", C.c_char_p, []),
     ("kbz_ctx_create", _vp, [_sz, _i, _sz]),
     ("kbz_ctx_destroy", None, [_vp]),
     ("kbz_set_ignore", _i, [_vp, _vp]),
@@ -49,6 +50,8 @@ SIGNATURES = [
     ("kbz_merge_and_device", _i, [_vp, _vp, _sz, _sz, _vp]),
     ("kbz_merge_and_host", _i, [_vp, _vp, _sz, _sz]),
     ("kbz_merge_and_fill", _i, [_vp, _sz, _sz, _vp, _vp]),
+    ("kbz_merge_and_fill_device", _i, [_vp, _sz, _sz, _vp, _vp, _vp]),
+    ("kbz_merge_and_fill_devices", _i, [_vp, _sz, _sz, _vp, _vp, _vp, _sz, _i, C.POINTER(_i)]),
     ("kbz_triage_modules_device", _i, [_vp, _sz, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("kbz_triage_modules_host", _i, [_vp, _sz, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp]),
     ("kbz_transform_rows_device", _i, [_vp, _sz, _sz, _sz, _i, _vp, _sz, _vp]),

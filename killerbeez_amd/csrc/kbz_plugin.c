@@ -98,6 +98,10 @@ typedef struct kbz_plugin {
   uint32_t *dprev;
   uint32_t *r_h32;         /* [nmod or 1][max_batch] hashes of the last window (dump_map_dir) */
   int restored_status;     /* last_process_status of a loaded state, until the next exec */
+  /* dynamorio_gpu: the first exec stands for the reference's first dynamorio_enable, whose
+   * setup_shm_and_pick_fuzzer_id(state, 1) resets the virgin maps (see dr_first_enable) */
+  int dr_enabled;
+  unsigned long dump_failures;  /* dump_map_dir / get_module_info bookkeeping that failed */
 } kbz_plugin_t;
 
 static size_t nmaps(const kbz_plugin_t *p) { return p->mode == KBZ_MODE_DYNAMORIO ? 1 : 3; }
@@ -694,35 +698,48 @@ static int sync_mirror(kbz_plugin_t *p) {
   return 0;
 }
 
+/* classify_counts (dynamorio_instrumentation.c:246-292: count_class_lookup8 over each byte) for
+ * the side outputs that need one classified map at a time -- a dump_map_dir file, get_module_info's
+ * info -- on the host: the novelty path itself never runs here. */
+static uint8_t g_cls8[256];
+static pthread_once_t g_cls_once = PTHREAD_ONCE_INIT;
+static void cls_table_init(void) {
+  for (int b = 0; b < 256; b++)
+    g_cls8[b] = b == 0 ? 0 : b == 1 ? 1 : b == 2 ? 2 : b == 3 ? 4 : b <= 7 ? 8 : b <= 15 ? 16
+                : b <= 31 ? 32 : b <= 127 ? 64 : 128;
+}
+static void classify_host(const uint8_t *in, uint8_t *out, size_t n) {
+  pthread_once(&g_cls_once, cls_table_init);
+  for (size_t i = 0; i < n; i++) out[i] = g_cls8[in[i]];
+}
+
 /* After a triaged window of n execs (rows of the k module maps back to back, `stride` apart):
  * remember the last exec's raw maps for get_module_info (dynamorio_instrumentation.c:1541-1573)
  * and, with dump_map_dir, write the classified map (has_new_coverage classifies trace_bits in
  * place, :1434) of every exec whose hash differs from the previous exec's -- the execs
  * has_new_coverage does not skip (:1450-1451) -- to <dir>/<%08x hash> (:1453-1458), in exec
  * order (a later exec with the same hash overwrites the file, as the reference's writes do).
- * The maps are classified on the GPU; p->r_h32 holds the window's hashes ([k][n]). */
-static int plugin_window_done(kbz_plugin_t *p, const uint8_t *rows, size_t n, size_t stride) {
+ * p->r_h32 holds the window's hashes ([k][n]); each dumped map is classified as it is written.
+ * Side outputs only: the window's results and tickets are already final when this runs, and a
+ * failure here (a full disk, host memory) is counted, never reported as a triage failure -- the
+ * reference ignores a failed write too. */
+static void plugin_window_done(kbz_plugin_t *p, const uint8_t *rows, size_t n, size_t stride) {
   const size_t k = p->per_module ? p->nmod : 1, m = p->map_size, row = k * m;
-  if (!n) return 0;
+  if (!n) return;
   p->have_exec = 1;
   p->gen++;
   if (p->per_module) {
     if (!p->last_raw && !(p->last_raw = (uint8_t *)malloc(row))) {
-      set_err("out of host memory");
-      return -1;
+      p->dump_failures++;
+      return;
     }
     memcpy(p->last_raw, rows + (n - 1) * stride, row);
   }
-  if (!p->dump_dir) return 0;
-  uint8_t *cls = (uint8_t *)malloc(n * row);
+  if (!p->dump_dir) return;
+  uint8_t *cls = (uint8_t *)malloc(m);
   if (!cls) {
-    set_err("out of host memory");
-    return -1;
-  }
-  if (kbz_transform_rows_host(rows, n, stride, row, KBZ_XF_CLASSIFY, cls, row)) {
-    set_err("GPU classify (dump_map_dir): %s", kbz_last_error());
-    free(cls);
-    return -1;
+    p->dump_failures++;
+    return;
   }
   for (size_t q = 0; q < k; q++) {
     uint32_t prev = p->dprev[q];
@@ -732,15 +749,51 @@ static int plugin_window_done(kbz_plugin_t *p, const uint8_t *rows, size_t n, si
       prev = h;
       char path[4096];
       snprintf(path, sizeof(path), "%s/%08x", p->dump_dir, h);
-      FILE *f = fopen(path, "wb");  /* the reference ignores a failed write too */
-      if (f) {
-        (void)fwrite(cls + j * row + q * m, 1, m, f);
-        fclose(f);
-      }
+      classify_host(rows + j * stride + q * m, cls, m);
+      FILE *f = fopen(path, "wb");
+      if (!f || fwrite(cls, 1, m, f) != m) p->dump_failures++;
+      if (f) fclose(f);
     }
     p->dprev[q] = prev;
   }
   free(cls);
+}
+
+/* The reference's first dynamorio_enable calls setup_shm_and_pick_fuzzer_id(state, 1)
+ * (dynamorio_instrumentation.c:1380-1382), which resets virgin_bits to 0xff (:496-497) -- and,
+ * with per_module_coverage, every module's map (:458-459, :474-475) -- even when create(options,
+ * state) or set_state loaded them; last_shm_hash (and last_path_was_new) are kept.  Here the first
+ * exec an instance records or triages stands for that enable.  A set_state after it keeps the
+ * loaded maps (fuzzer_id is set by then), and a create + merge with no exec never resets.  The AFL
+ * plugin keeps loaded maps: its setup_shm only fills maps it allocates (afl_instrumentation.c:
+ * 553-559). */
+static int dr_first_enable(kbz_plugin_t *p) {
+  if (p->mode != KBZ_MODE_DYNAMORIO || p->dr_enabled) return 0;
+  const size_t m = p->map_size;
+  if (p->per_module) {
+    memset(p->mvirgin, 0xff, p->nmod * m);
+    uint8_t *v3 = (uint8_t *)malloc(3 * m);
+    if (!v3) {
+      set_err("out of host memory");
+      return -1;
+    }
+    memset(v3, 0xff, 3 * m);
+    for (size_t i = 0; i < p->nmod; i++) {
+      if (p->mctx[i] && kbz_set_virgin(p->mctx[i], v3)) {
+        set_err("GPU state upload: %s", kbz_last_error());
+        free(v3);
+        return -1;
+      }
+    }
+    free(v3);
+  } else {
+    memset(p->virgin, 0xff, 3 * m);
+    if (p->ctx && kbz_set_virgin(p->ctx, p->virgin)) {
+      set_err("GPU state upload: %s", kbz_last_error());
+      return -1;
+    }
+  }
+  p->dr_enabled = 1;
   return 0;
 }
 
@@ -768,11 +821,12 @@ static int plugin_flush(kbz_plugin_t *p) {
     set_err("GPU triage: %s", kbz_last_error());
     return -1;
   }
-  if (plugin_window_done(p, rows, n, (p->per_module ? p->nmod : 1) * p->map_size)) return -1;
+  /* the window's results and tickets first: the side outputs below cannot undo them */
   p->last_path_was_new = p->r_hnb[n - 1] != 0;
   p->r_base = p->q_base;
   p->r_n = n;
   p->q_base += (long)n;
+  plugin_window_done(p, rows, n, (p->per_module ? p->nmod : 1) * p->map_size);
   return 0;
 }
 
@@ -787,6 +841,7 @@ static long plugin_record(kbz_plugin_t *p, const uint8_t *trace, int fuzz_result
     return -1;
   }
   if (p->q_rows && p->q_n == p->q_cap && plugin_flush(p)) return -1;
+  if (dr_first_enable(p)) return -1;
   if (p->per_module && !p->q_rows) {  /* module maps back to back: nmod * map_size bytes */
     if (ensure_ctx(p)) return -1;
     p->q_rows = p->mq;
@@ -833,7 +888,9 @@ static int plugin_triage_batch(kbz_plugin_t *p, const uint8_t *traces, size_t n,
     set_err("bad arguments (null traces or stride < the exec's map bytes)");
     return -1;
   }
-  if (plugin_flush(p) || ensure_ctx(p)) return -1; /* queued execs come first */
+  if (plugin_flush(p)) return -1; /* queued execs come first */
+  if (n && dr_first_enable(p)) return -1;
+  if (ensure_ctx(p)) return -1;
   p->mirror_stale = 1;
   if (p->per_module) {  /* hnb = the exec's result over all modules (0/1) */
     if (h32 || x64) {
@@ -851,7 +908,7 @@ static int plugin_triage_batch(kbz_plugin_t *p, const uint8_t *traces, size_t n,
         return -1;
       }
       for (size_t i = 0; i < p->nmod; i++) p->mnew[i] = p->r_mhnb[i * cnt + cnt - 1] != 0;
-      if (plugin_window_done(p, traces + lo * stride, cnt, stride)) return -1;
+      plugin_window_done(p, traces + lo * stride, cnt, stride);
     }
     return 0;
   }
@@ -866,7 +923,7 @@ static int plugin_triage_batch(kbz_plugin_t *p, const uint8_t *traces, size_t n,
       return -1;
     }
     if (p->dump_dir && hb != p->r_h32) memcpy(p->r_h32, hb, cnt * sizeof(uint32_t));
-    if (plugin_window_done(p, traces + lo * stride, cnt, stride)) return -1;
+    plugin_window_done(p, traces + lo * stride, cnt, stride);
   }
   return 0;
 }
@@ -899,14 +956,11 @@ static int plugin_module_info(kbz_plugin_t *p, int index, int *is_new, char **mo
     if (info) {
       const size_t row = p->nmod * m;
       if (p->cls_gen != p->gen || !p->last_cls) {
-        if (!p->last_cls && !(p->last_cls = (uint8_t *)malloc(row))) {
+        if (!p->last_raw || (!p->last_cls && !(p->last_cls = (uint8_t *)malloc(row)))) {
           set_err("out of host memory");
           return -1;
         }
-        if (kbz_transform_rows_host(p->last_raw, 1, row, row, KBZ_XF_CLASSIFY, p->last_cls, row)) {
-          set_err("GPU classify: %s", kbz_last_error());
-          return -1;
-        }
+        classify_host(p->last_raw, p->last_cls, row);  /* one exec's maps: no GPU round trip */
         p->cls_gen = p->gen;
       }
       *info = (char *)p->last_cls + (size_t)index * m;
@@ -1196,15 +1250,20 @@ static int json_hex_fast(const char *json, const char *key, uint8_t *out, size_t
   return hex_decode(v + 1, out, n);
 }
 
-typedef struct {
+typedef struct {             /* one merge_files call */
   const kbz_plugin_t *cfg;   /* options of the merge (mode, map_size, modules) */
   const char *const *paths;
   size_t row;                /* bytes per state row */
-  uint8_t *dst;              /* current slot */
-  size_t first, count, next;
+  size_t threads;            /* decoding threads per fill call */
   pthread_mutex_t mu;
   int failed;
   char err[512];
+} files_ctx_t;
+typedef struct {             /* one fill call: a slot of states [first, first + count) */
+  files_ctx_t *ctx;
+  uint8_t *dst;
+  size_t first, count, next;
+  pthread_mutex_t mu;
 } files_job_t;
 
 static char *read_text_file(const char *path) {
@@ -1227,7 +1286,7 @@ static char *read_text_file(const char *path) {
 }
 
 /* one file -> one row; returns 0 or writes a message to err */
-static int decode_state_file(const files_job_t *j, const char *path, uint8_t *row, char *err,
+static int decode_state_file(const files_ctx_t *j, const char *path, uint8_t *row, char *err,
                              size_t errn) {
   const kbz_plugin_t *c = j->cfg;
   const size_t m = c->map_size;
@@ -1287,36 +1346,92 @@ static int decode_state_file(const files_job_t *j, const char *path, uint8_t *ro
 
 static void *files_worker(void *arg) {
   files_job_t *j = (files_job_t *)arg;
+  files_ctx_t *c = j->ctx;
   char err[512];
   for (;;) {
     pthread_mutex_lock(&j->mu);
-    const size_t i = j->failed ? j->count : j->next++;
+    const size_t i = j->next++;
     pthread_mutex_unlock(&j->mu);
-    if (i >= j->count) return NULL;
-    if (decode_state_file(j, j->paths[j->first + i], j->dst + i * j->row, err, sizeof(err))) {
-      pthread_mutex_lock(&j->mu);
-      if (!j->failed) memcpy(j->err, err, sizeof(err));
-      j->failed = 1;
-      pthread_mutex_unlock(&j->mu);
+    pthread_mutex_lock(&c->mu);
+    const int failed = c->failed;
+    pthread_mutex_unlock(&c->mu);
+    if (i >= j->count || failed) return NULL;
+    if (decode_state_file(c, c->paths[j->first + i], j->dst + i * c->row, err, sizeof(err))) {
+      pthread_mutex_lock(&c->mu);
+      if (!c->failed) memcpy(c->err, err, sizeof(err));
+      c->failed = 1;
+      pthread_mutex_unlock(&c->mu);
       return NULL;
     }
   }
 }
 
+/* kbz_merge_and_fill(_devices) callback: decode states [first, first + count) into dst.  With
+ * several GPUs the workers call it concurrently for disjoint ranges: everything it changes is per
+ * call, except the shared failure record (under ctx->mu). */
 static int fill_from_files(void *user, uint8_t *dst, size_t first, size_t count) {
-  files_job_t *j = (files_job_t *)user;
-  j->dst = dst;
-  j->first = first;
-  j->count = count;
-  j->next = 0;
+  files_job_t j;
+  j.ctx = (files_ctx_t *)user;
+  j.dst = dst;
+  j.first = first;
+  j.count = count;
+  j.next = 0;
+  pthread_mutex_init(&j.mu, NULL);
   enum { kMaxThreads = 16 };
   pthread_t th[kMaxThreads];
-  size_t nt = count < kMaxThreads ? count : kMaxThreads, started = 0;
+  size_t nt = j.ctx->threads < kMaxThreads ? j.ctx->threads : kMaxThreads, started = 0;
+  if (nt > count) nt = count;
   for (; started < nt; started++)
-    if (pthread_create(&th[started], NULL, files_worker, j)) break;
-  if (started == 0) files_worker(j);  /* no threads available: decode on the caller */
+    if (pthread_create(&th[started], NULL, files_worker, &j)) break;
+  if (started == 0) files_worker(&j);  /* no threads available: decode on the caller */
   for (size_t t = 0; t < started; t++) pthread_join(th[t], NULL);
-  return j->failed;
+  pthread_mutex_destroy(&j.mu);
+  pthread_mutex_lock(&j.ctx->mu);
+  const int failed = j.ctx->failed;
+  pthread_mutex_unlock(&j.ctx->mu);
+  return failed;
+}
+
+/* merge_devices option: absent = the current GPU (one fold); an array of device ordinals (a device
+ * may repeat) or "all" = every visible GPU: kbz_merge_and_fill_devices.  0 ok (*ndev 0 = absent),
+ * -1 malformed. */
+static int parse_merge_devices(const char *options, int **devs, size_t *ndev, int *all) {
+  *devs = NULL;
+  *ndev = 0;
+  *all = 0;
+  const char *v = options ? json_value(options, "merge_devices") : NULL;
+  if (!v) return 0;
+  if (*v == '"') {
+    char *sv = json_unquote(v);
+    const int ok = sv && !strcmp(sv, "all");
+    free(sv);
+    if (!ok) return -1;
+    *all = 1;
+    return 0;
+  }
+  size_t n = 0;
+  int bad = 0;
+  char **items = json_array(options, "merge_devices", &n, &bad);
+  if (bad || !items || !n || n > 64) {
+    free_strings(items, n);
+    return -1;
+  }
+  int *d = (int *)malloc(n * sizeof(int));
+  for (size_t i = 0; d && i < n; i++) {
+    char *e = NULL;
+    const long x = strtol(items[i], &e, 10);
+    if (!e || *e || e == items[i] || x < 0 || x > 1024) {
+      free(d);
+      d = NULL;
+    } else {
+      d[i] = (int)x;
+    }
+  }
+  free_strings(items, n);
+  if (!d) return -1;
+  *devs = d;
+  *ndev = n;
+  return 0;
 }
 
 static kbz_plugin_t *plugin_merge_files(int mode, const char *options, const char *const *paths,
@@ -1332,16 +1447,32 @@ static kbz_plugin_t *plugin_merge_files(int mode, const char *options, const cha
     }
   kbz_plugin_t *r = plugin_from_options(mode, options);
   if (!r) return NULL;
+  int *devs = NULL, all = 0;
+  size_t ndev = 0;
+  if (parse_merge_devices(options, &devs, &ndev, &all)) {
+    set_err("merge_devices must be \"all\" or an array of GPU ordinals");
+    plugin_free(r);
+    return NULL;
+  }
   pthread_once(&g_hex_once, hex_table_init);
   const size_t k = r->per_module ? r->nmod : nmaps(r);
-  files_job_t j;
+  files_ctx_t j;
   memset(&j, 0, sizeof(j));
   j.cfg = r;
   j.paths = paths;
   j.row = k * r->map_size;
+  /* 16 decoding threads in all, shared by the GPU workers */
+  const size_t workers = all ? 8 : ndev ? ndev : 1;
+  j.threads = workers >= 8 ? 2 : 16 / workers;
   pthread_mutex_init(&j.mu, NULL);
   uint8_t *out = (uint8_t *)malloc(j.row);
-  int rc = out ? kbz_merge_and_fill(out, n, j.row, fill_from_files, &j) : -1;
+  int rc = -1;
+  if (out && (all || ndev))  /* the node's GPUs: merger/merger.c's fold sharded across them */
+    rc = kbz_merge_and_fill_devices(out, n, j.row, fill_from_files, &j, all ? NULL : devs,
+                                    ndev, KBZ_EXCHANGE_AUTO, NULL);
+  else if (out)
+    rc = kbz_merge_and_fill(out, n, j.row, fill_from_files, &j);
+  free(devs);
   pthread_mutex_destroy(&j.mu);
   if (rc) {
     if (!out) set_err("out of host memory");
@@ -1360,7 +1491,9 @@ static const char kHelpAfl[] =
     "afl_gpu - AFL bitmap triage (has_new_bits vs virgin_bits/tmout/crash) on the GPU\n"
     "Options:\n"
     "  map_size              Trace map size in bytes (default 65536)\n"
-    "  max_batch             Execs triaged per GPU batch (default 4096)\n";
+    "  max_batch             Execs triaged per GPU batch (default 4096)\n"
+    "  merge_devices         merge_files: \"all\" or an array of GPU ordinals to shard the\n"
+    "                        fold over (default: the current GPU)\n";
 static const char kHelpDr[] =
     "dynamorio_gpu - DynamoRIO/winafl triage (classify_counts, hash32, last-hash skip,\n"
     "                has_new_bits) on the GPU\n"
@@ -1373,7 +1506,9 @@ static const char kHelpDr[] =
     "  coverage_modules      Array of module names (per_module_coverage)\n"
     "  ignore_bytes_dir      Directory of <module>.dat ignore bytes files (per_module_coverage)\n"
     "  dump_map_dir          Directory: every exec that is not a last-hash skip writes its\n"
-    "                        classified map to <dir>/<hash32 as %08x>\n";
+    "                        classified map to <dir>/<hash32 as %08x>\n"
+    "  merge_devices         merge_files: \"all\" or an array of GPU ordinals to shard the\n"
+    "                        fold over (default: the current GPU)\n";
 
 static int plugin_help(int mode, char **help_str) {
   if (!help_str) return -1;

@@ -287,9 +287,6 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #ifndef KBZ_SROWS_MAX
 #define KBZ_SROWS_MAX 16  // 8, 16, 32 equal at 2 % hangs + crashes; 4 is slower (profiles/r02_v19)
 #endif
-#ifndef KBZ_PASS1_LMIX4  // k_pass1s wave L: mixes of 4 words at once, ahead of their chain steps
-#define KBZ_PASS1_LMIX4 0  // 1: 0.83 vs 0.80 ms (VALU), profiles/r03_v10
-#endif
 #ifndef KBZ_PASS1_LPRE  // k_pass1s wave L: iterations (2 LDS slots each) read ahead (1 or 2)
 #define KBZ_PASS1_LPRE 1
 #endif
@@ -346,10 +343,8 @@ struct Pass1Args {
 // row-per-lane ds_read_b128 are both bank-conflict-free.  Raw zero words stay 0 in LDS; a
 // simplified trace's transformed word is never 0, so L maps an untouched 0 of a simplified
 // lane to 0x0101010101010101.
-// ABL (timing-only ablation builds, never used for results): 1 = T skips its per-word work,
-// 2 = L skips its chains, 3 = both.
 // ---------------------------------------------------------------------------------------------
-template <int MODE, bool IGN, bool X64, int ABL = 0, int D = 4>
+template <int MODE, bool IGN, bool X64, int D>
 __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   constexpr int NC = (MODE == KBZ_MODE_DYNAMORIO) ? 1 : 3;
   // AFL mode: wave T also computes the hash32 mix of every word it transforms and leaves it in
@@ -417,10 +412,6 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
     uint64_t x0 = kXP1 + kXP2, x1 = kXP2, x2 = 0, x3 = 0 - kXP1;
     const uint64_t ksimp = h32_mix(kSimpleZero);
     auto chain_tile = [&](uint32_t t, int b) {
-      if (ABL & 2) {
-        asm volatile("" ::"v"(lds[b * TILE + lane].x));
-        return;
-      }
       const uint64_t *ig = IGN ? (const uint64_t *)(a.ignore + (size_t)t * TW) : nullptr;
       const uint4 *row = &lds[b * TILE + lane * SLOTS];
       const int sw = lane & 15;
@@ -432,38 +423,6 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         // software pipeline: the next LP x 2 slots are in flight while these 4 words chain
         const int qn = (q + 2 * LP) & (SLOTS - 1);
         const uint4 n0 = row[qn ^ sw], n1 = row[(qn + 1) ^ sw];
-        if (KBZ_PASS1_LMIX4 && !TMIX) {
-          // the 4 words' mixes are independent of the chain: computed together, ahead of the 4
-          // steps (one ballot per group; h32_mix(0) = 0), so the chain waits on no mix
-          const uint64_t wv[4] = {ld_u64(v0, 0), ld_u64(v0, 1), ld_u64(v1, 0), ld_u64(v1, 1)};
-          uint64_t tv[4], kv[4];
-          if (__ballot((wv[0] | wv[1] | wv[2] | wv[3]) != 0)) {
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-              tv[j] = (simp && wv[j] == 0) ? kSimpleZero : wv[j];
-              kv[j] = h32_mix_mad(tv[j] & (IGN ? ig[2 * q + j] : ~0ull));
-            }
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-              tv[j] = simp ? kSimpleZero : 0;
-              kv[j] = simp ? ksimp : 0;
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            h = h32_step_fast(h, kv[j]);
-            if (X64) {
-              const int xl = j & 3;
-              if (xl == 0) x0 = xx_round(x0, tv[j]);
-              else if (xl == 1) x1 = xx_round(x1, tv[j]);
-              else if (xl == 2) x2 = xx_round(x2, tv[j]);
-              else x3 = xx_round(x3, tv[j]);
-            }
-          }
-          if (LP > 1) { v0 = u0; v1 = u1; u0 = n0; u1 = n1; } else { v0 = n0; v1 = n1; }
-          continue;
-        }
 #pragma unroll
         for (int qq = 0; qq < 2; qq++) {
           const uint4 v = qq ? v1 : v0;
@@ -622,7 +581,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
 #pragma unroll
       for (int j = 0; j < TP; j++) vring[j] = row[j ^ sw];
 #pragma unroll 1
-      for (int q0 = 0; q0 < ((ABL & 1) ? 0 : SLOTS); q0 += TP)
+      for (int q0 = 0; q0 < SLOTS; q0 += TP)
 #pragma unroll
       for (int u = 0; u < TP; u++) {
         const int q = q0 + u;
@@ -861,9 +820,7 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
 #pragma unroll
         for (int u = 0; u < D; u++) {
           const uint32_t s = g + u;
-#ifndef KBZ_XP_NOCHAIN
           if (isL && s >= 3 && s - 3 < ntiles) chain_tile(s - 3);
-#endif
           KBZ_STAMP(0);
           vmcnt_wait_ring<(D - 1) * NLD>(R[u]);
           KBZ_STAMP(2);
@@ -976,9 +933,6 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
 #pragma unroll
       for (int i = 0; i < RG; i++) {
         tw[i] = xw[b][i];
-#ifdef KBZ_XP_NOCLS
-        if (MODE == KBZ_MODE_DYNAMORIO) continue;
-#endif
         const uint32_t c = (clsw >> (2 * i)) & 3;
         if (MODE == KBZ_MODE_DYNAMORIO) tw[i] = classify8(tw[i]);
         else if (c != 0) tw[i] = simplify8(tw[i]);
@@ -992,11 +946,7 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
       char *kb = (char *)&kbuf[b * TILE];
 #pragma unroll
       for (int i = 0; i < RG; i++) {
-#ifdef KBZ_XP_NOMIX
-        *(uint64_t *)(kb + adr[i]) = tw[i] & igw;
-#else
         *(uint64_t *)(kb + adr[i]) = h32_mix_mad(tw[i] & igw);
-#endif
       }
       uint64_t ow[NC];
 #pragma unroll
@@ -1179,9 +1129,6 @@ __device__ __forceinline__ u32x4 simp_or(u32x4 o, u32x4 z) {
   return nz | ((~z >> 7) & 0x01010101u);
 }
 
-#ifndef KBZ_N_ABL  // timing-only ablations of k_pass1n (wrong results): 1 = no simplified-class
-#define KBZ_N_ABL 0  // reduce, 2 = no class-0 reduce
-#endif
 template <int MODE, int NW, int D>
 __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
   static_assert(MODE != KBZ_MODE_DYNAMORIO, "DynamoRIO always hashes (last-hash skip)");
@@ -1240,10 +1187,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
   const uint32_t rlast = (uint32_t)((nrows - 1) * a.stride);
   // branch-free asm loads (see k_pass1s); tiles past t1 re-load tile t0
   auto load = [&](u32x4 (&r)[NR], uint32_t t) {
-    uint32_t tt = t < t1 ? t : t0;
-#ifdef KBZ_N_RR  // timing-only experiment: the same work, tiles dealt round-robin to the waves
-    tt = ((tt - t0) * NW + wave) % ntiles;
-#endif
+    const uint32_t tt = t < t1 ? t : t0;
 #pragma unroll
     for (int i = 0; i < NLD; i++) {
       const uint32_t off = min((uint32_t)(i * rstep + lr * a.stride), rlast);
@@ -1268,7 +1212,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
       // ---- column ORs of tile t over the chunk's rows, per class
       u32x4 o0 = {0, 0, 0, 0};
 #pragma unroll
-      for (int i = 0; i < ((KBZ_N_ABL & 2) ? 0 : NLD); i++) {
+      for (int i = 0; i < NLD; i++) {
         u32x4 x = R[u][i];
         if (MODE == KBZ_MODE_AFL_CLASSIFY)
           x = u32x4{classify4(x.x), classify4(x.y), classify4(x.z), classify4(x.w)};
@@ -1279,7 +1223,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
 #pragma unroll
       for (int k = 1; k < NC; k++) {
         fin[k] = u32x4{0, 0, 0, 0};
-        if (!present[k] || (KBZ_N_ABL & 1)) continue;  // wave-uniform, per chunk
+        if (!present[k]) continue;  // wave-uniform, per chunk
         u32x4 ok = {0, 0, 0, 0}, zk = {~0u, ~0u, ~0u, ~0u};
 #pragma unroll
         for (int i = 0; i < NLD; i++) {
@@ -1362,19 +1306,10 @@ __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
 #ifndef KBZ_MAX_FW
 #define KBZ_MAX_FW 1024  // tile-flag words per class: maps up to 16 MiB
 #endif
-#ifndef KBZ_PASS1D_ABL  // timing-only ablations (wrong results), bits: 1 = C skips the chain,
-                        // 2 = N only hands slots back, 4 = X skips classify, 8 = X skips the mix
-#define KBZ_PASS1D_ABL 0
-#endif
-#ifndef KBZ_PASS1D_CN  // 1: without ignore bytes C runs the neighbour test itself, in its chain's
-#define KBZ_PASS1D_CN 0   // dependency bubbles (wave 4 idles with NX = 6, is an X wave with NX = 7)
-#endif
 template <bool IGN, bool X64, int NX, int RING, int D>
 __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
   // X waves are the waves off SIMD 0 (3 of every 4): wave 0 is C, wave 4 is N, wave 8 idles
   static_assert(NX == 6 || NX == 9, "6 or 9 X waves: 8 or 12 waves per workgroup");
-  // CN: C tests neighbours on its k words (wave 4 then idles)
-  constexpr bool CN = KBZ_PASS1D_CN && !IGN;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = kChunk / RPI;
   constexpr int NR = NLD + 1 + (IGN ? 1 : 0);  // rows, virgin words, ignore words
   constexpr int TILE = kChunk * SLOTS;          // uint4 per ring slot
@@ -1421,30 +1356,17 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
 #pragma unroll
       for (int q = 0; q < SLOTS; q++) kb[b][q] = kring[sl * TILE + lane * SLOTS + (q ^ sw)];
     };
-    uint32_t nacc_lo = 0, nacc_hi = 0;  // CN: OR over the row's words of (word ^ previous row's)
     // chain the tile in kb[b] (slot sl); tile t + 1's words (slot sl + 1) are read meanwhile, one
     // ds_read_b128 per two steps (in the chain's dependency gaps, not as a burst of 16)
     auto chain = [&](auto bc, auto sc) {
       constexpr int b = decltype(bc)::value, sl = decltype(sc)::value, sl1 = (sl + 1) % RING;
-      if (!(KBZ_PASS1D_ABL & 1)) {
 #pragma unroll
-        for (int q = 0; q < SLOTS; q++) {
-          kb[b ^ 1][q] = kring[sl1 * TILE + lane * SLOTS + (q ^ sw)];
-          __builtin_amdgcn_sched_barrier(0);
-          const uint4 kq = kb[b][q];
-          h = h32_step_fast(h, (uint64_t)kq.x | ((uint64_t)kq.y << 32));
-          h = h32_step_fast(h, (uint64_t)kq.z | ((uint64_t)kq.w << 32));
-          if (CN) {  // 32-bit halves: wave_shr:1 with bound_ctrl (lane 0 reads 0)
-            nacc_lo |= (kq.x ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)kq.x, 0x138, 0xf, 0xf, true)) |
-                       (kq.z ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)kq.z, 0x138, 0xf, 0xf, true));
-            nacc_hi |= (kq.y ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)kq.y, 0x138, 0xf, 0xf, true)) |
-                       (kq.w ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)kq.w, 0x138, 0xf, 0xf, true));
-            asm volatile("" : "+v"(nacc_lo), "+v"(nacc_hi));  // ORed now, not deferred (spills)
-          }
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < SLOTS; q++) h ^= kb[b][q].x;
+      for (int q = 0; q < SLOTS; q++) {
+        kb[b ^ 1][q] = kring[sl1 * TILE + lane * SLOTS + (q ^ sw)];
+        __builtin_amdgcn_sched_barrier(0);
+        const uint4 kq = kb[b][q];
+        h = h32_step_fast(h, (uint64_t)kq.x | ((uint64_t)kq.y << 32));
+        h = h32_step_fast(h, (uint64_t)kq.z | ((uint64_t)kq.w << 32));
       }
       if (X64) {
 #pragma unroll 4
@@ -1518,13 +1440,9 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
         a.shard_last[1] = 1;
       }
     }
-    if (CN && lane < nrows) a.neq[row0 + lane] = (nacc_lo | nacc_hi) != 0;  // lane 0: placeholder, as N's
     if (lane == 0) a.chunk_cls[chunk] = 1;  // DynamoRIO: one virgin map, every row in it
-  } else if (wave == 4 && !CN) {
+  } else if (wave == 4) {
     // ------------------------------------------------------------ N: the neighbour test
-#ifdef KBZ_PASS1D_NPRIO  // timing-only A/B
-    __builtin_amdgcn_s_setprio(KBZ_PASS1D_NPRIO);
-#endif
     uint64_t nacc = 0;  // OR over the row's words of (word ^ previous row's word)
     const uint4 *ring = IGN ? wring : kring;
     for (uint32_t t0 = 0; t0 < ntiles; t0 += RING)
@@ -1533,10 +1451,6 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
       const uint32_t t = t0 + sl;
       if (t >= ntiles) return;
       wait_ready(t);
-      if (KBZ_PASS1D_ABL & 2) {
-        if (lane == 0) KBZ_FST(freed_n, sl, (int)t);
-        return;
-      }
       uint4 vv[SLOTS];
 #pragma unroll
       for (int q = 0; q < SLOTS; q++) vv[q] = ring[sl * TILE + lane * SLOTS + (q ^ sw)];
@@ -1552,13 +1466,10 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
     // lane 0 has no predecessor in the wave: a placeholder (k_skip compares chunk starts)
     if (lane < nrows) a.neq[row0 + lane] = nacc != 0;
   } else if ((wave & 3) == 0) {
-    // idle (wave 8; wave 4 with CN): SIMD 0 is left to the chain
+    // idle (wave 8): SIMD 0 is left to the chain
   } else {
     // ------------------------------------------------------------ X waves
     const int xi = wave - 1 - wave / 4;  // 0..NX-1
-#ifdef KBZ_PASS1D_XPRIO  // timing-only A/B: the younger X waves of each SIMD at raised priority
-    if (wave >= 4) __builtin_amdgcn_s_setprio(KBZ_PASS1D_XPRIO);
-#endif
     const int lr = lane / SLOTS, ls = lane % SLOTS;
     const uint8_t *cbase = a.traces + row0 * a.stride;  // the chunk's rows: < 64 x 32 MiB
     const uint32_t rstep = (uint32_t)(RPI * a.stride);
@@ -1598,8 +1509,7 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
 #pragma unroll
         for (int i = 0; i < NLD; i++) {
           const u32x4 x = R[u][i];
-          if (!(KBZ_PASS1D_ABL & 4))
-            R[u][i] = u32x4{classify4(x.x), classify4(x.y), classify4(x.z), classify4(x.w)};
+          R[u][i] = u32x4{classify4(x.x), classify4(x.y), classify4(x.z), classify4(x.w)};
           o |= R[u][i];
         }
         o = or_lanes(o);
@@ -1615,7 +1525,7 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
         const int sl = (int)(t % RING);
         KBZ_STAMP(1);
         if (mine)  // the slot is free once C and N have read tile t - RING from it
-          while (KBZ_FLD(freed_c, sl) != (int)t - RING || (!CN && KBZ_FLD(freed_n, sl) != (int)t - RING))
+          while (KBZ_FLD(freed_c, sl) != (int)t - RING || KBZ_FLD(freed_n, sl) != (int)t - RING)
             __builtin_amdgcn_s_sleep(1);
         asm volatile("" ::: "memory");
         KBZ_STAMP(2);
@@ -1629,8 +1539,8 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
             const uint64_t c1 = (uint64_t)c.z | ((uint64_t)c.w << 32);
             const uint64_t g0 = (uint64_t)igw.x | ((uint64_t)igw.y << 32);
             const uint64_t g1 = (uint64_t)igw.z | ((uint64_t)igw.w << 32);
-            const uint64_t k0 = (KBZ_PASS1D_ABL & 8) ? c0 & g0 : h32_mix_mad(c0 & g0);
-            const uint64_t k1 = (KBZ_PASS1D_ABL & 8) ? c1 & g1 : h32_mix_mad(c1 & g1);
+            const uint64_t k0 = h32_mix_mad(c0 & g0);
+            const uint64_t k1 = h32_mix_mad(c1 & g1);
             kring[idx] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1,
                                     (uint32_t)(k1 >> 32));
             if (IGN) {  // the neighbour test looks at the bytes whose ignore byte is 0
@@ -1955,12 +1865,8 @@ struct ItemStage {
   uint64_t *buf;  // this wave's LDS staging area, kWaveItems entries
   uint32_t n;     // wave-uniform fill
 };
-#ifndef KBZ_SCAN_ABL  // timing-only ablations (wrong results): 1 = no claim items, 2 = items
-#define KBZ_SCAN_ABL 0   // staged but never appended to the global list
-#endif
 __device__ __forceinline__ void flush_items(ItemStage &st, uint64_t *items, uint32_t cap,
                                             uint32_t *counters) {
-  if (KBZ_SCAN_ABL & 2) st.n = 0;
   if (!st.n) return;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's staged writes are done
   uint32_t base = 0;
@@ -2239,7 +2145,7 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
         if (!st[u]) o[u] = make_uint4(0, 0, 0, 0);  // nothing still virgin in that tile
         const uint4 nb = make_uint4(o[u].x & vr.x & ~prev.x, o[u].y & vr.y & ~prev.y,
                                     o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
-        if (!(KBZ_SCAN_ABL & 1) && __ballot(nb.x | nb.y | nb.z | nb.w)) {  // wave-uniform
+        if (__ballot(nb.x | nb.y | nb.z | nb.w)) {  // wave-uniform
           if (KBZ_SCAN_INLINE && wave_claimed_bytes(nb) < win_items)
             claims_enqueue(ca, k, cq, c, col, nb, vir, prev);
           else
@@ -2806,9 +2712,9 @@ constexpr int kWideNX = KBZ_WIDE_NX;        // transform waves of k_pass1w
 constexpr int kWideNL = KBZ_WIDE_NL;        // loader waves of k_pass1w
 constexpr int kWideD = KBZ_WIDE_D;          // their register ring depth
 constexpr uint32_t kWideBelowChunks = 512;  // 2 chunks per CU on a 256-CU MI355X
-#ifndef KBZ_EVENT_SCOPE  // timing-only A/B builds: 0 = default (system-scope) event fences
-#define KBZ_EVENT_SCOPE hipEventReleaseToDevice
-#endif
+// pass-1 / stage timing events: device-scope release (the default system-scope fence costs
+// ~6 us of idle GPU per event, profiles/r02_v9)
+constexpr unsigned kEventScope = hipEventReleaseToDevice;
 #ifndef KBZ_PASS1_DEPTH
 #define KBZ_PASS1_DEPTH 2
 #endif
@@ -2816,22 +2722,10 @@ constexpr uint32_t kWideBelowChunks = 512;  // 2 chunks per CU on a 256-CU MI355
 // context forces one (kbz_ctx_set_pass1; the environment KBZ_PASS1=narrow|wide sets a new
 // context's default, for A/B timing).
 bool pass1_is_wide(int choice, uint32_t chunks) {
-#ifdef KBZ_ABLATION
-  return false;
-#else
   if (choice == KBZ_PASS1_NARROW) return false;
   if (choice == KBZ_PASS1_WIDE) return true;
   return chunks < kWideBelowChunks;
-#endif
 }
-#ifdef KBZ_ABLATION
-template <int MODE, bool IGN, bool X64, int ABL>
-void launch_abl(int depth, const Pass1Args &a, uint32_t chunks, hipStream_t s) {
-  if (depth == 2) hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, ABL, 2>), dim3(chunks), dim3(128), 0, s, a);
-  else if (depth == 3) hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, ABL, 3>), dim3(chunks), dim3(128), 0, s, a);
-  else hipLaunchKernelGGL((k_pass1s<MODE, IGN, X64, ABL, 4>), dim3(chunks), dim3(128), 0, s, a);
-}
-#endif
 // Pass-1 launches.  With timing on (kbz_ctx_time_pass1) the kernel is dispatched by
 // hipExtLaunchKernelGGL with start/stop events taken from its own dispatch packet: no marker
 // packets around it (two hipEventRecord calls left ~6 us of idle GPU each between pass 1 and
@@ -2846,9 +2740,6 @@ void p1_launch(K kernel, dim3 grid, dim3 block, hipStream_t s, const P1Ev &ev, c
   else
     hipLaunchKernelGGL(kernel, grid, block, 0, s, a);
 }
-#ifndef KBZ_PASS1D  // timing-only A/B builds: 0 = the lock-step k_pass1w for wide DynamoRIO batches
-#define KBZ_PASS1D 1
-#endif
 #ifndef KBZ_PASS1D_D
 #define KBZ_PASS1D_D 2
 #endif
@@ -2860,18 +2751,7 @@ void p1_launch(K kernel, dim3 grid, dim3 block, hipStream_t s, const P1Ev &ev, c
 #endif
 template <int MODE, bool IGN, bool X64>
 void launch_pass1(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s, const P1Ev &ev) {
-#ifdef KBZ_ABLATION
-  // timing-only builds: KBZ_ABL selects the ablation, KBZ_DEPTH the register ring depth
-  static const int abl = getenv("KBZ_ABL") ? atoi(getenv("KBZ_ABL")) : 0;
-  static const int depth = getenv("KBZ_DEPTH") ? atoi(getenv("KBZ_DEPTH")) : KBZ_PASS1_DEPTH;
-  (void)choice;
-  (void)ev;
-  if (abl == 1) return launch_abl<MODE, IGN, X64, 1>(depth, a, chunks, s);
-  if (abl == 2) return launch_abl<MODE, IGN, X64, 2>(depth, a, chunks, s);
-  if (abl == 3) return launch_abl<MODE, IGN, X64, 3>(depth, a, chunks, s);
-  return launch_abl<MODE, IGN, X64, 0>(depth, a, chunks, s);
-#else
-  if (KBZ_PASS1D && MODE == KBZ_MODE_DYNAMORIO && pass1_is_wide(choice, chunks)) {
+  if (MODE == KBZ_MODE_DYNAMORIO && pass1_is_wide(choice, chunks)) {
     constexpr int RING = (IGN && X64) ? 2 : (IGN || X64) ? 3 : KBZ_PASS1D_RING;
     constexpr int NW = KBZ_PASS1D_NX / 3 * 4;
     p1_launch(k_pass1d<IGN, X64, KBZ_PASS1D_NX, RING, KBZ_PASS1D_D>, dim3(chunks), dim3(64 * NW),
@@ -2880,8 +2760,7 @@ void launch_pass1(int choice, const Pass1Args &a, uint32_t chunks, hipStream_t s
     p1_launch(k_pass1w<MODE, IGN, X64, kWideNX, kWideNL, kWideD>, dim3(chunks),
               dim3(64 * (kWideNL + kWideNX)), s, ev, a);
   else
-    p1_launch(k_pass1s<MODE, IGN, X64, 0, KBZ_PASS1_DEPTH>, dim3(chunks), dim3(128), s, ev, a);
-#endif
+    p1_launch(k_pass1s<MODE, IGN, X64, KBZ_PASS1_DEPTH>, dim3(chunks), dim3(128), s, ev, a);
 }
 
 #ifndef KBZ_PASS1N_D  // register ring depth of k_pass1n, narrow (2 waves per chunk) / wide (8)
@@ -2940,7 +2819,7 @@ int stage_begin(kbz_ctx *c, hipStream_t s, hipEvent_t *out) {
   if (c->ev_pool_used + 2 > c->ev_pool.size()) {
     for (int i = 0; i < 2; i++) {
       hipEvent_t e;
-      HIP_TRY(hipEventCreateWithFlags(&e, KBZ_EVENT_SCOPE));
+      HIP_TRY(hipEventCreateWithFlags(&e, kEventScope));
       c->ev_pool.push_back(e);
     }
   }
@@ -2968,6 +2847,10 @@ int check_rows(const void *p, size_t stride, size_t M) {
 extern "C" {
 
 int kbz_abi_version(void) { return KBZ_ABI_VERSION; }
+#ifndef KBZ_BUILD_FLAGS_STR  // set by killerbeez_amd/build.py: "" for the product library
+#define KBZ_BUILD_FLAGS_STR "unrecorded: built outside killerbeez_amd/build.py"
+#endif
+const char *kbz_build_flags(void) { return KBZ_BUILD_FLAGS_STR; }
 const char *kbz_last_error(void) { return g_err.c_str(); }
 
 kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
@@ -3209,20 +3092,14 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
       std::pair<hipEvent_t, hipEvent_t> e;
       // device-scope release: the default system-scope fence adds ~13 us per batch on MI355X
       // (same-box A/B, profiles/r02_v9)
-      HIP_TRY(hipEventCreateWithFlags(&e.first, KBZ_EVENT_SCOPE));
-      HIP_TRY(hipEventCreateWithFlags(&e.second, KBZ_EVENT_SCOPE));
+      HIP_TRY(hipEventCreateWithFlags(&e.first, kEventScope));
+      HIP_TRY(hipEventCreateWithFlags(&e.second, kEventScope));
       c->ev_pass1.push_back(e);
     }
     pev.start = c->ev_pass1[c->ev_used_n].first;
     pev.stop = c->ev_pass1[c->ev_used_n++].second;
-#ifdef KBZ_ABLATION  // timing-only builds launch through launch_abl: marker events around it
-    HIP_TRY(hipEventRecord(pev.start, s));
-#endif
   }
   if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, hashed, s, pev)) return -1;
-#ifdef KBZ_ABLATION
-  if (pev.stop) HIP_TRY(hipEventRecord(pev.stop, s));
-#endif
   if (c->mode == KBZ_MODE_DYNAMORIO) {  // the skip rule for rows j >= 1 needs no other shard
     hipEvent_t st0;
     if (stage_begin(c, s, &st0)) return -1;
@@ -3461,9 +3338,6 @@ int kbz_sync(kbz_ctx_t *c, void *stream) {
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   uint32_t cnt[4];
   HIP_TRY(hipMemcpy(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost));
-#if defined(KBZ_XP_NOMIX) || defined(KBZ_XP_NOCLS) || KBZ_PASS1D_ABL
-  cnt[1] = cnt[2] = 0;  // timing-only builds with inconsistent results
-#endif
   if (cnt[1] || cnt[2]) {  // sticky until reported here
     HIP_TRY(hipMemset(c->counters + 1, 0, 2 * sizeof(uint32_t)));
     c->h_err[0] = c->h_err[1] = 0;  // k_pack's host-mapped copy: reported now, not again
@@ -3745,7 +3619,7 @@ namespace {
 struct MergeStaging {
   hipStream_t cs = nullptr, ws = nullptr;
   uint8_t *pin[2] = {nullptr, nullptr}, *dst[2] = {nullptr, nullptr};
-  uint8_t *acc = nullptr, *part = nullptr;
+  uint8_t *part = nullptr;
   hipEvent_t copied[2] = {nullptr, nullptr}, used[2] = {nullptr, nullptr};
   ~MergeStaging() {
     if (ws) (void)hipStreamSynchronize(ws);
@@ -3756,7 +3630,6 @@ struct MergeStaging {
       if (copied[i]) (void)hipEventDestroy(copied[i]);
       if (used[i]) (void)hipEventDestroy(used[i]);
     }
-    if (acc) (void)hipFree(acc);
     if (part) (void)hipFree(part);
     if (cs) (void)hipStreamDestroy(cs);
     if (ws) (void)hipStreamDestroy(ws);
@@ -3764,12 +3637,15 @@ struct MergeStaging {
 };
 }  // namespace
 
-int kbz_merge_and_fill(uint8_t *out, size_t n, size_t state_bytes, kbz_merge_fill_fn fill,
-                       void *user) {
-  if (!out || (!fill && n)) return fail("null argument");
+// The fold of kbz_merge_and_fill with its result left in device memory d_out (state_bytes,
+// current device), ordered on `stream` (the library's own streams do the copies and folds).
+int kbz_merge_and_fill_device(uint8_t *d_out, size_t n, size_t state_bytes, kbz_merge_fill_fn fill,
+                              void *user, void *stream) {
+  if (!d_out || (!fill && n)) return fail("null argument");
   if (state_bytes == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
   if (n == 0) {
-    memset(out, 0xff, state_bytes);
+    HIP_TRY(hipMemsetAsync(d_out, 0xff, state_bytes, s));
     return 0;
   }
   // slots of up to 256 MiB: the caller fills slot b while the GPU copies and folds slot b ^ 1
@@ -3784,9 +3660,15 @@ int kbz_merge_and_fill(uint8_t *out, size_t n, size_t state_bytes, kbz_merge_fil
     HIP_TRY(hipEventCreateWithFlags(&m.copied[i], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&m.used[i], hipEventDisableTiming));
   }
-  HIP_TRY(hipMalloc((void **)&m.acc, state_bytes));
   HIP_TRY(hipMalloc((void **)&m.part, state_bytes));
-  HIP_TRY(hipMemsetAsync(m.acc, 0xff, state_bytes, m.ws));
+  // the caller's stream may still be using d_out: the fold starts after it
+  hipEvent_t ready = nullptr;
+  HIP_TRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+  const hipError_t er = hipEventRecord(ready, s);
+  const hipError_t ew = er == hipSuccess ? hipStreamWaitEvent(m.ws, ready, 0) : er;
+  (void)hipEventDestroy(ready);
+  HIP_TRY(ew);
+  HIP_TRY(hipMemsetAsync(d_out, 0xff, state_bytes, m.ws));
   for (size_t lo = 0, b = 0; lo < n; lo += cap, b++) {
     const int sl = (int)(b & 1);
     const size_t cnt = std::min(cap, n - lo);
@@ -3796,20 +3678,42 @@ int kbz_merge_and_fill(uint8_t *out, size_t n, size_t state_bytes, kbz_merge_fil
     HIP_TRY(hipEventRecord(m.copied[sl], m.cs));
     HIP_TRY(hipStreamWaitEvent(m.ws, m.copied[sl], 0));
     if (kbz_merge_and_device(m.part, m.dst[sl], cnt, state_bytes, m.ws)) return -1;
-    if (state_bytes % 16 == 0) {
+    if (state_bytes % 16 == 0 && ((uintptr_t)d_out & 15) == 0) {
       hipLaunchKernelGGL(k_and_rows, dim3(cdiv(state_bytes / 16, 256)), dim3(256), 0, m.ws, m.part,
-                         (size_t)1, state_bytes, m.acc, 1);
+                         (size_t)1, state_bytes, d_out, 1);
     } else {
       hipLaunchKernelGGL(k_and_bytes, dim3(cdiv(state_bytes, 256)), dim3(256), 0, m.ws, m.part,
-                         (size_t)1, state_bytes, m.acc, 1);
+                         (size_t)1, state_bytes, d_out, 1);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(m.used[sl], m.ws));
   }
+  // the caller's stream continues after the fold (m's streams are synchronised and destroyed
+  // on return, so this wait is already satisfied when it is queued)
   HIP_TRY(hipStreamSynchronize(m.ws));
-  HIP_TRY(hipMemcpy(out, m.acc, state_bytes, hipMemcpyDeviceToHost));
   return 0;
 }
+
+int kbz_merge_and_fill(uint8_t *out, size_t n, size_t state_bytes, kbz_merge_fill_fn fill,
+                       void *user) {
+  if (!out || (!fill && n)) return fail("null argument");
+  if (state_bytes == 0) return 0;
+  if (n == 0) {
+    memset(out, 0xff, state_bytes);
+    return 0;
+  }
+  uint8_t *acc = nullptr;
+  HIP_TRY(hipMalloc((void **)&acc, state_bytes));
+  int rc = kbz_merge_and_fill_device(acc, n, state_bytes, fill, user, nullptr);
+  if (!rc && hipMemcpy(out, acc, state_bytes, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail("kbz_merge_and_fill: copy of the result failed");
+  (void)hipFree(acc);
+  return rc;
+}
+
+// Internal (not in the header): kbz_multi.hip's worker threads hand their error message to the
+// calling thread through it.
+void kbz__set_error(const char *msg) { g_err = msg ? msg : ""; }
 
 namespace {
 struct HostRows {

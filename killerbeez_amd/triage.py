@@ -321,6 +321,42 @@ def merge_and_host(states: np.ndarray) -> np.ndarray:
     return out
 
 
+EXCHANGE_AUTO, EXCHANGE_COPY, EXCHANGE_RCCL = 0, 1, 2
+_FILL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t)
+
+
+def merge_and_devices(states: np.ndarray, devices=None, exchange: int = EXCHANGE_AUTO):
+    """The merger fold sharded over GPUs from C (kbz_merge_and_fill_devices): host states
+    [n, state_bytes] are handed to the workers through the fill callback (called from the
+    library's worker threads).  devices: ordinals (a device may repeat) or None = every visible
+    GPU.  Returns (merged state, exchange used)."""
+    s = np.ascontiguousarray(states, dtype=np.uint8)
+    n = s.shape[0]
+    nbytes = s[0].size if n else (s.shape[1] if s.ndim == 2 else 0)
+    flat = s.reshape(n, nbytes)
+
+    def fill(_user, dst, first, count):
+        try:
+            C.memmove(dst, flat[first:first + count].ctypes.data, count * nbytes)
+            return 0
+        except Exception:  # noqa: BLE001 - reported to the library as a failed fill
+            return 1
+
+    cb = _FILL_FN(fill)
+    out = np.empty(nbytes, np.uint8)
+    used = C.c_int(-1)
+    if devices is None:
+        dev_arr, ndev = None, 0
+    else:
+        dev_arr = (C.c_int * len(devices))(*devices)
+        ndev = len(devices)
+    check(lib().kbz_merge_and_fill_devices(_np_ptr(out), n, nbytes, C.cast(cb, C.c_void_p), None,
+                                           C.cast(dev_arr, C.c_void_p) if dev_arr is not None
+                                           else None, ndev, exchange, C.byref(used)),
+          "kbz_merge_and_fill_devices")
+    return out, used.value
+
+
 def triage_modules(ctxs, traces, offsets, outcome=None, stream=None, hashes=False):
     """DynamoRIO per-module coverage (has_new_coverage_per_module,
     dynamorio_instrumentation.c:1477-1493) over an ordered batch.  ctxs: one TriageContext per

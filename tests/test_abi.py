@@ -57,3 +57,40 @@ def test_plugin_layout_matches_reference_header(tmp_path):
     subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Werror", "-I", ref, "-I", kbuild.INC,
                            src, "-o", str(exe)])
     assert subprocess.call([str(exe)]) == 0
+
+
+def test_product_library_has_no_experiment_flags():
+    """The shipped libkbz_hip.so is the plain product build: kbz_build_flags() is empty (timing
+    variants and diagnostics live only in build_variants/, and report their -D flags)."""
+    L = C.CDLL(kbuild.HIP_LIB)
+    L.kbz_build_flags.restype = C.c_char_p
+    assert L.kbz_build_flags() == b""
+    if not os.environ.get("KBZ_HIP_LIB"):
+        assert _lib.lib().kbz_build_flags() == b""
+
+
+def test_product_build_refuses_extra_flags(monkeypatch):
+    monkeypatch.setenv("KBZ_HIPCC_FLAGS", "-DKBZ_STAMPS")
+    with pytest.raises(kbuild.BuildError):
+        kbuild.build_hip()
+
+
+def test_build_is_redone_when_the_command_changes(tmp_path):
+    """The stamp is a digest of the compile command and of every source: a different flag set
+    makes the library stale even when no source is newer than it."""
+    out = str(tmp_path / "lib.so")
+    src = tmp_path / "a.c"
+    src.write_text("int f(void) { return 1; }\n")
+    cmd = ["gcc", "-shared", "-fPIC", str(src), "-o", out + ".tmp"]
+    kbuild._run(out, cmd, [str(src)], False)
+    assert kbuild._up_to_date(out, cmd, [str(src)])
+    assert not kbuild._up_to_date(out, cmd + ["-DX=1"], [str(src)])
+    src.write_text("int f(void) { return 2; }\n")
+    assert not kbuild._up_to_date(out, cmd, [str(src)])
+
+
+def test_variant_flags_are_checked():
+    with pytest.raises(kbuild.BuildError):
+        kbuild.build_variant("bad", ["-O0"])
+    with pytest.raises(kbuild.BuildError):
+        kbuild.build_variant("bad", ['-DX="y"'])

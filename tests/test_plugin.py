@@ -221,8 +221,11 @@ def test_state_load_continue_and_merge(gpu, name, mode):
     # -isf/-isd style: dump, load into a new state, continue (fuzzer/main.c:300-322, :426-436)
     b = P.Plugin(name, f'{{"map_size": {M}}}', a.get_state())
     r = b.triage_batch(t[100:], oc[100:])
-    whole = _expected(mode, t, oc)
-    np.testing.assert_array_equal(r["hnb"], whole["hnb"][100:])
+    if name == "afl_gpu":  # the loaded maps carry on (afl_instrumentation.c:553-559)
+        np.testing.assert_array_equal(r["hnb"], _expected(mode, t, oc)["hnb"][100:])
+    else:  # the first exec's enable resets virgin_bits, keeps the hash (test_dynamorio_resume)
+        last = P.state_maps(a.get_state(), M)["last_shm_hash"]
+        np.testing.assert_array_equal(r["hnb"], _expected(mode, t[100:], oc[100:], last=last)["hnb"])
     # merger: AND of the maps (afl_merge :123-140, dynamorio_merge :1180-1231)
     c = P.Plugin(name, f'{{"map_size": {M}}}')
     c.triage_batch(t[50:], oc[50:])
@@ -335,6 +338,82 @@ def test_config1_real_traces_per_exec(gpu, name, mode):
         p.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("per_module", [False, True])
+def test_dynamorio_resume(gpu, per_module):
+    """A resumed DynamoRIO campaign (fuzzer -isf: create(options, state), then execs).  The
+    reference's first dynamorio_enable calls setup_shm_and_pick_fuzzer_id(state, 1)
+    (dynamorio_instrumentation.c:1380-1382), which resets virgin_bits to 0xff (:496-497; every
+    module's map with per_module_coverage, :458-459, :474-475) and keeps last_shm_hash.  So the
+    per-exec results equal the oracle run from all-0xff maps with the restored hash; a set_state
+    after an exec keeps the loaded maps; create + merge with no exec keeps them too."""
+    import json
+
+    n = 90
+    mods = MODS if per_module else ["x"]
+    k = len(mods)
+    parts = [synth.sparse_np(2 * n, M, seed=80 + i, hot_frac=0.05)[0] for i in range(k)]
+    for part in parts:
+        part[n] = part[n - 1]  # the first resumed exec repeats the saved campaign's last exec
+        part[n + 5:n + 9] = part[n + 4]
+    rows = np.concatenate(parts, axis=1)
+    opts = (PM_OPTS % (M, json.dumps(MODS))) if per_module else f'{{"map_size": {M}, "max_batch": 16}}'
+    a = P.Plugin("dynamorio_gpu", opts)
+    a.triage_batch(rows[:n], hashes=False)
+    st = a.get_state()
+    saved = P.state_maps(st, M)
+    lasts = ([saved["modules"][nm]["last_shm_hash"] for nm in mods] if per_module
+             else [saved["last_shm_hash"]])
+    maps = ([saved["modules"][nm]["virgin_bits"] for nm in mods] if per_module
+            else [saved["virgin_bits"]])
+    assert all((mp != 0xFF).any() for mp in maps)  # the saved maps are not fresh
+    exp = [oracle.triage_batch(oracle.MODE_DYNAMORIO, parts[i][n:], None, last_hash=lasts[i])
+           for i in range(k)]
+    # the saved maps would give other results: the reset is what makes these match
+    old = [oracle.triage_batch(oracle.MODE_DYNAMORIO, parts[i][n:], None, last_hash=lasts[i],
+                               virgin=np.stack([maps[i]] * 3)) for i in range(k)]
+    want = np.any([e["hnb"] != 0 for e in exp], axis=0)
+    assert not np.array_equal(want, np.any([e["hnb"] != 0 for e in old], axis=0))
+    # create(options, state) then execs one at a time (fuzzer/main.c:374-385)
+    b = P.Plugin("dynamorio_gpu", opts, st)
+    for j in range(n):
+        assert b.record(rows[n + j], P.FUZZ_NONE) == j
+        assert b.is_new_path() == int(want[j]), j
+    got = P.state_maps(b.get_state(), M)
+    for i, nm in enumerate(mods):
+        g = got["modules"][nm] if per_module else got
+        np.testing.assert_array_equal(g["virgin_bits"], exp[i]["virgin"][0])
+        assert g["last_shm_hash"] == exp[i]["last_hash"]
+    # set_state after the first exec: the loaded maps are kept (fuzzer_id is set by then)
+    b.set_state(st)
+    r = b.triage_batch(rows[n:], hashes=False)
+    np.testing.assert_array_equal(r["hnb"], np.any([e["hnb"] != 0 for e in old], axis=0))
+    # the batched member resets too, on its first exec
+    c = P.Plugin("dynamorio_gpu", opts, st)
+    np.testing.assert_array_equal(c.triage_batch(rows[n:], hashes=False)["hnb"], want)
+    # no exec, no enable: a loaded state merges with its maps
+    d = P.Plugin("dynamorio_gpu", opts, st)
+    m = d.merge(P.Plugin("dynamorio_gpu", opts))
+    got = P.state_maps(m.get_state(), M)
+    for i, nm in enumerate(mods):
+        np.testing.assert_array_equal((got["modules"][nm] if per_module else got)["virgin_bits"],
+                                      maps[i])
+
+
+@pytest.mark.gpu
+def test_afl_resume_keeps_loaded_maps(gpu):
+    """afl_gpu: a loaded state's three maps carry on into the next execs
+    (afl_instrumentation.c:553-559 fills only the maps it allocates)."""
+    t, oc = synth.sparse_np(160, M, seed=81, hot_frac=0.05, outcome_p=(0.8, 0.1, 0.1))
+    a = P.Plugin("afl_gpu", f'{{"map_size": {M}, "max_batch": 16}}')
+    a.triage_batch(t[:80], oc[:80])
+    b = P.Plugin("afl_gpu", f'{{"map_size": {M}, "max_batch": 16}}', a.get_state())
+    exp = _expected(oracle.MODE_AFL, t, oc)
+    for j in range(80, 160):
+        b.record(t[j], int(oc[j]))
+        assert b.is_new_path() == int(exp["hnb"][j] != 0), j
+
+
 # ---- dynamorio_gpu per_module_coverage (dynamorio_instrumentation.c:1048-1063, :1477-1493) ----
 
 MODS = ["target.exe", "lib_a.dll", "lib b.dll"]
@@ -394,10 +473,12 @@ def test_per_module_coverage_plugin(gpu, tmp_path):
         np.testing.assert_array_equal(got[name]["virgin_bits"], exp[i]["virgin"][0])
         assert got[name]["last_shm_hash"] == exp[i]["last_hash"]
         assert got[name]["last_path_was_new"] == int(exp[i]["hnb"][n - 1] != 0)
-    # dump -> load into a new state -> the next execs continue from it
+    # dump -> load into a new state -> the next execs continue from it: every module's map is
+    # reset by the first exec's enable (dynamorio_instrumentation.c:458-459, :474-475), its last
+    # hash is kept
     q = P.Plugin("dynamorio_gpu", opts, st)
     exp2 = [oracle.triage_batch(oracle.MODE_DYNAMORIO, parts[i][n:], None, ignore=igs[i],
-                                virgin=exp[i]["virgin"], last_hash=exp[i]["last_hash"])
+                                last_hash=exp[i]["last_hash"])
             for i in range(k)]
     res = q.triage_batch(rows[n:], hashes=False)
     np.testing.assert_array_equal(res["hnb"], np.any([e["hnb"] != 0 for e in exp2], axis=0))
