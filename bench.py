@@ -67,6 +67,9 @@ def parse():
     p.add_argument("--no-pmc", dest="pmc", action="store_false",
                    help="skip the live roofline.traffic measurement (two rocprofv3 --pmc passes "
                         "of a short child run, rank 0 with 1 GPU) and report the stored one")
+    p.add_argument("--no-ktrace", dest="ktrace", action="store_false",
+                   help="skip the rocprofv3 --kernel-trace child run behind roofline.rocprof "
+                        "(rank 0 with 1 GPU)")
     p.add_argument("--seed", type=int, default=0x5EED)
     p.add_argument("--workload", default="config2",
                    choices=["config2", "config3", "merge", "stream", "plugin"])
@@ -216,8 +219,16 @@ def cpu_baseline(traces_dev, outcome_dev, mode, seconds):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
+    flags = ""
+    if kind == "reference":
+        try:
+            rf = oracle.ref().ref_build_flags
+            rf.restype = C.c_char_p
+            flags = f", reference built with gcc {rf().decode()}"
+        except AttributeError:
+            flags = ", reference build flags unrecorded"
     return {"value": round(done / el, 1), "unit": "traces/s", "cores": 1, "kind": kind,
-            "sample": f"{sample_n} traces x {m} B of the bench workload, {passes} sequential "
+            "sample": f"{sample_n} traces x {m} B of the bench workload{flags}, {passes} sequential "
                       f"passes ({el:.1f} s), virgin carried, 1 thread"}
 
 
@@ -290,6 +301,68 @@ def live_traffic(args, warmup=1, steps=4):
             "source": f"live rocprofv3 --pmc, {len(fetch)} fresh-batch dispatches: "
                       f"FETCH_SIZE x2 = {2.0 * med(fetch) * 1024:.0f} B + WRITE_SIZE = "
                       f"{med(write) * 1024:.0f} B"}
+
+
+def live_kernel_trace(args, warmup=3, steps=12):
+    """The roofline's kernel time from the profiler: a rocprofv3 --kernel-trace child run of the
+    same workload (no variants, no PMC); its timed steps' pass-1 dispatches are the last `steps`
+    pass-1 dispatches of the trace.  Returns their average duration (and min / max), the child's
+    own ms_per_step and HIP-event pass-1 time, and every kernel of those steps (start relative to
+    the step's pass 1, duration), also written to $KBZ_BENCH_KTRACE_OUT (a JSON the evidence
+    script commits under profiles/) -- so the line's `frac` can be recomputed from profiles/."""
+    import csv
+    import glob
+    import tempfile
+
+    wa = ["--workload", args.workload, "--mode", args.mode, "--batch", str(args.batch),
+          "--map-size", str(args.map_size), "--warmup", str(warmup), "--steps", str(steps),
+          "--seed", str(args.seed), *(["--hash"] if args.hash else [])]
+    with tempfile.TemporaryDirectory() as d:
+        cmd = ["rocprofv3", "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run",
+               "--", sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-variants",
+               "--no-pmc", "--no-ktrace", *wa]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, check=True)
+        child = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+        rows = []
+        for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+            for row in csv.DictReader(open(f)):
+                name = row.get("Kernel_Name", "")
+                if "(anonymous namespace)::k_" not in name:
+                    continue
+                k = name.split("(anonymous namespace)::")[1].split("(")[0].split("<")[0]
+                rows.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), k))
+    rows.sort()
+    p1 = [i for i, x in enumerate(rows) if x[2].startswith("k_pass1")]
+    if len(p1) < steps:
+        return None
+    first = p1[-steps]
+    timed = [i for i in p1 if i >= first]
+    durs = [(rows[i][1] - rows[i][0]) / 1e6 for i in timed]
+    per_step = []
+    for si, i in enumerate(timed):
+        nxt = timed[si + 1] if si + 1 < len(timed) else len(rows)
+        t0 = rows[i][0]
+        per_step.append([{"kernel": rows[j][2], "start_us": round((rows[j][0] - t0) / 1e3, 2),
+                          "dur_us": round((rows[j][1] - rows[j][0]) / 1e3, 2)}
+                         for j in range(i, nxt)])
+    span = [(rows[timed[si + 1]][0] - rows[i][0]) / 1e6 for si, i in enumerate(timed[:-1])]
+    avg = sum(durs) / len(durs)
+    out = {"avg_ms": round(avg, 4), "min_ms": round(min(durs), 4), "max_ms": round(max(durs), 4),
+           "dispatches": len(durs),
+           "child_ms_per_step": child.get("ms_per_step"),
+           "child_hip_event_avg_ms": child.get("roofline", {}).get("avg_launch_ms"),
+           "median_step_span_ms": round(sorted(span)[len(span) // 2], 4) if span else None,
+           "what": f"rocprofv3 --kernel-trace of a child run of this workload ({warmup} warmup + "
+                   f"{steps} timed fresh batches); the last {steps} pass-1 dispatches = its timed "
+                   "steps; step span = pass-1 start to the next pass-1 start"}
+    dest = os.environ.get("KBZ_BENCH_KTRACE_OUT")
+    if dest:
+        os.makedirs(os.path.dirname(os.path.abspath(dest)), exist_ok=True)
+        json.dump(dict(out, workload=args.workload, mode=args.mode, batch=args.batch,
+                       map_size=args.map_size, pass1_durations_ms=[round(x, 5) for x in durs],
+                       steps=per_step), open(dest, "w"), indent=1)
+        out["trace_file"] = dest
+    return out
 
 
 # A/B only: KBZ_BENCH_P1_TIMING=0 times the steps without the pass-1 events (roofline invalid)
@@ -549,6 +622,12 @@ def main_triage(args):
             traffic = {"bytes": None, "source": f"live PMC failed: {type(e).__name__}"}
     if traffic is None:
         traffic = stored_traffic(args.workload) or {"bytes": None, "source": "none"}
+    ktrace = None
+    if rank == 0 and world == 1 and args.ktrace:
+        try:
+            ktrace = live_kernel_trace(args, steps=min(args.steps, 12))
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal
+            ktrace = {"avg_ms": None, "what": f"kernel trace failed: {type(e).__name__}: {e}"[:300]}
     valu = None
     if rank == 0 and world == 1 and args.pmc and dense:
         try:
@@ -595,6 +674,12 @@ def main_triage(args):
         "pass1_share_of_step": round(pass1_ms / ms_per_step, 4),
         "variants": variants,
     }
+    if ktrace:
+        if ktrace.get("avg_ms"):
+            res["roofline"]["rocprof_avg_ms"] = ktrace["avg_ms"]
+            res["roofline"]["rocprof_frac"] = round(B * M / (ktrace["avg_ms"] * 1e-3) / 1e9
+                                                    / HBM_PEAK_GBS, 4)
+        res["roofline"]["rocprof"] = ktrace
     if valu and valu.get("instructions_per_launch"):
         valu["frac"] = round(valu["floor_ms"] / pass1_ms, 4)
         valu["bound"] = "valu"
@@ -776,7 +861,7 @@ def main_stream(args):
         _, _, x64, o = item
         keys = torch.from_numpy(np.stack([x64.view(np.int64), o.astype(np.int64)], 1)).to(dev)
         mask = torch.from_numpy(o != 0).to(dev)
-        n_new += int(dedup_sharded(table, keys, mask, rank, world).sum().item())
+        n_new = n_new + dedup_sharded(table, keys, mask, rank, world).sum()  # no host sync
 
     def step(i):
         r, o = ctx.ring_acquire()  # waits for this slot's previous batch: its results are in
@@ -824,7 +909,7 @@ def main_stream(args):
            "pcie_h2d_peak_GBps": pcie,
            "pcie_frac": round(gbps / pcie["value"], 4),
            "xxh64_table_insert": ins,
-           "unique_crash_hang_keys": table.size(), "new_keys_reported": n_new}
+           "unique_crash_hang_keys": table.size(), "new_keys_reported": int(n_new)}
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()

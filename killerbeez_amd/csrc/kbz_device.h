@@ -43,14 +43,6 @@ KBZ_HD uint32_t bitrev32(uint32_t x) {
 // (The round-1 form, a 3-step smear of the highest bit, was 13 instructions:
 // tools/valuprobe.hip.)
 KBZ_HD uint32_t classify4(uint32_t x) {
-#ifdef KBZ_CLASSIFY_SMEAR  // timing-only A/B builds (scripts/build_variants.sh): the 13-instruction form
-  const uint32_t y1 = x << 1, y2 = x << 2;
-  const uint32_t y = (x | (y1 & 0x78787878u)) | (y2 & y1 & 0x04040404u);
-  uint32_t s = y | ((y >> 1) & 0x7F7F7F7Fu);
-  s |= (s >> 2) & 0x3F3F3F3Fu;
-  s |= (s >> 4) & 0x0F0F0F0Fu;
-  return s ^ ((s >> 1) & 0x7F7F7F7Fu);
-#endif
   const uint32_t x1 = (x << 1) | 0x01010101u;                 // v_lshl_or_b32
 #if defined(__HIP_DEVICE_COMPILE__)
   uint32_t m;  // one v_and_or_b32 (the compiler emits v_and + v_or); one SGPR operand at most

@@ -233,6 +233,29 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 #define KBZ_STAMP(i) do {} while (0)
 #define KBZ_STAMP_FLUSH(slot) do {} while (0)
 #endif
+// Diagnostic build only (-DKBZ_TAIL_STAMPS): per-wave records of the tail kernels (100-MHz
+// s_memrealtime at entry / after the prologue / at exit, work counters), read back by
+// tools/tail_stamps.py through kbz_debug_tail().  No record is written otherwise.
+#ifdef KBZ_TAIL_STAMPS
+constexpr int kTailRecs = 1 << 16;
+__device__ unsigned long long g_kbz_tail[kTailRecs * 4];
+__device__ __forceinline__ unsigned long long rt_now() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+#define KBZ_TAIL_DECL unsigned long long tl_t0 = rt_now(), tl_t1 = 0; uint32_t tl_walk = 0, tl_claims = 0, tl_flush = 0, tl_win = 0
+#define KBZ_TAIL_MARK() (tl_t1 = rt_now())
+#define KBZ_TAIL_ADD(f, v) (tl_##f += (v))
+#define KBZ_TAIL_END(id) do { const unsigned long long _e = rt_now(); const uint32_t _i = (id); \
+    if ((threadIdx.x & 63) == 0 && _i < (uint32_t)kTailRecs) { g_kbz_tail[_i * 4] = tl_t0; g_kbz_tail[_i * 4 + 1] = tl_t1 ? tl_t1 : _e; \
+    g_kbz_tail[_i * 4 + 2] = _e; g_kbz_tail[_i * 4 + 3] = ((unsigned long long)tl_walk << 48) | ((unsigned long long)(tl_claims & 0xffff) << 32) | ((tl_flush & 0xffff) << 16) | (tl_win & 0xffff); } } while (0)
+#else
+#define KBZ_TAIL_DECL do {} while (0)
+#define KBZ_TAIL_MARK() do {} while (0)
+#define KBZ_TAIL_ADD(f, v) do {} while (0)
+#define KBZ_TAIL_END(id) do {} while (0)
+#endif
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
@@ -2056,6 +2079,8 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
                                                const uint32_t *listed, uint32_t win_items,
                                                ClaimArgs ca) {
   // no per-lane early return: every lane of a wave takes part in the item-allocation prefix
+  KBZ_TAIL_DECL;
+  const uint32_t tail_id = ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6);
   const uint32_t col0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
   const bool live = col0 < map_size;
   const uint32_t col = live ? col0 : 0;
@@ -2107,7 +2132,11 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
   ClaimQ cq{claim_q[threadIdx.x >> 6], 0};
   const uint32_t seg_new = (send.x & vr.x & ~prev.x) | (send.y & vr.y & ~prev.y) |
                            (send.z & vr.z & ~prev.z) | (send.w & vr.w & ~prev.w);
-  if (!__ballot(seg_new != 0)) return;  // wave-uniform: nothing new in this segment
+  KBZ_TAIL_MARK();
+  if (!__ballot(seg_new != 0)) {  // wave-uniform: nothing new in this segment
+    KBZ_TAIL_END(tail_id);
+    return;
+  }
   // Only chunks that hold traces of class k AND stored (or, DynamoRIO fix path, recomputed) one
   // of this wave's 4 tiles can add bits here: an unstored tile held no still-virgin bit, so a
   // skipped chunk changes neither the claims nor the running OR.  Lane l tests chunk cg + l;
@@ -2122,6 +2151,7 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
       any = (listed && listed[cl]) ||
             ((tflags[((size_t)cl * nclass + k) * nfw + (t0 >> 6)] >> (t0 & 63)) & 0xFull);
     uint64_t mask = __ballot(any);
+    KBZ_TAIL_ADD(walk, (uint32_t)__popcll(mask));
     while (mask) {
       uint32_t cs[KBZ_SCAN_ILP];
 #pragma unroll
@@ -2146,12 +2176,16 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
         const uint4 nb = make_uint4(o[u].x & vr.x & ~prev.x, o[u].y & vr.y & ~prev.y,
                                     o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
         if (__ballot(nb.x | nb.y | nb.z | nb.w)) {  // wave-uniform
-          if (KBZ_SCAN_INLINE && wave_claimed_bytes(nb) < win_items)
+          const uint32_t ncl = wave_claimed_bytes(nb);
+          if (KBZ_SCAN_INLINE && ncl < win_items) {
+            KBZ_TAIL_ADD(claims, ncl);
             claims_enqueue(ca, k, cq, c, col, nb, vir, prev);
-          else
+          } else {
+            KBZ_TAIL_ADD(win, 1);
             emit_items_wave(c, k, col, nb, vir, prev, stg, items, cap, counters,
                             (uint8_t *)chunk_or + (size_t)c * nclass * map_size + kc, live,
                             win_items);
+          }
         }
         prev = or4(prev, o[u]);
       }
@@ -2159,6 +2193,7 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
   }
   claims_flush(ca, k, cq);
   flush_items(stg, items, cap, counters);
+  KBZ_TAIL_END(tail_id);
 }
 
 // Window item: lane l owns 16-B column group l of the chunk's 1-KiB window; the rows of the
@@ -2306,6 +2341,116 @@ __global__ void k_pack(uint32_t *hnb32, const uint32_t *h32, uint32_t n, uint8_t
   if (hnb_out) hnb_out[j] = (uint8_t)hnb32[j];
   if (h32_out) h32_out[j] = h32[j];
   hnb32[j] = 0;  // ready for the next batch
+}
+
+// ---------------------------------------------------------------------------------------------
+// Small AFL-mode batches without hashes in ONE launch (the AFL plugin's per-exec flushes:
+// fuzzer/main.c:385 asks is_new_path after every exec; afl_instrumentation.c:231-274 routes each
+// exec's map by outcome and runs has_new_bits, :600-662, on it).  With n <= 64 traces every
+// workgroup owns a slice of the map's columns for ALL rows of the batch, so the sequential rule
+// needs no other workgroup: lane = 16-B column group, rows in order with the three virgin maps
+// in registers -- row j claims t_j & V_k (k = its class), scores 2 where it has a nonzero byte
+// whose V_k byte is 0xff, V_k &= ~t_j.  Per row the workgroup's best score meets in LDS, then one
+// agent-scope atomicMax per (workgroup, row) into hnb32; the last workgroup to finish (an agent
+// atomic ticket after a release fence) packs hnb32 into hnb_out and re-arms it.  Rows are read 16
+// at a time (from pinned host memory on the plugin's zero-copy path).
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kSmallRows = 64;
+struct SmallArgs {
+  const uint8_t *traces;
+  size_t stride;
+  uint32_t n, map_size;
+  const int8_t *outcome;
+  const uint8_t *vcur;
+  uint8_t *vnext;
+  uint32_t *hnb32;
+  uint8_t *hnb_out;
+  uint32_t *ticket;    // zero between launches (the last workgroup re-arms it)
+  uint32_t *stats;     // kbz_ctx_stats words of the batch (counters[8..10])
+};
+__device__ __forceinline__ uint4 xform16(uint4 a, int xf) {
+  const uint64_t lo = xform8((uint64_t)a.x | ((uint64_t)a.y << 32), xf);
+  const uint64_t hi = xform8((uint64_t)a.z | ((uint64_t)a.w << 32), xf);
+  return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+template <int MODE>
+__global__ __launch_bounds__(256) void k_small(SmallArgs a) {
+  static_assert(MODE != KBZ_MODE_DYNAMORIO, "DynamoRIO hashes every trace (k_pass1*)");
+  __shared__ uint32_t score[kSmallRows];
+  __shared__ int last;
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x < kSmallRows) score[threadIdx.x] = 0;
+  const uint32_t n = a.n;
+  // lane j: row j's class (rows are wave-uniform below: readlane)
+  const int clsl = class_of(MODE, (lane < (int)n && a.outcome) ? a.outcome[lane] : KBZ_FUZZ_NONE);
+  const uint32_t col0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  const bool live = col0 < a.map_size;
+  const uint32_t col = live ? col0 : 0;
+  uint4 v[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) v[k] = *(const uint4 *)(a.vcur + (size_t)k * a.map_size + col);
+  if (!live)
+#pragma unroll
+    for (int k = 0; k < 3; k++) v[k] = make_uint4(0, 0, 0, 0);  // no claim from a dead lane
+  __syncthreads();  // score[] is zero
+  constexpr int G = 16;  // rows in flight per lane
+  for (uint32_t j0 = 0; j0 < n; j0 += G) {
+    uint4 r[G];
+#pragma unroll
+    for (int u = 0; u < G; u++) {
+      const uint32_t j = min(j0 + u, n - 1);  // past the end: a valid row, not processed
+      r[u] = *(const uint4 *)(a.traces + (size_t)j * a.stride + col);
+    }
+#pragma unroll
+    for (int u = 0; u < G; u++) {
+      const uint32_t j = j0 + u;
+      if (j >= n) break;  // uniform
+      const int k = __builtin_amdgcn_readlane(clsl, j);
+      const uint4 t = xform16(r[u], class_xf(MODE, k));
+      uint4 vk = k == 0 ? v[0] : k == 1 ? v[1] : v[2];
+      const uint64_t t0 = (uint64_t)t.x | ((uint64_t)t.y << 32), t1 = (uint64_t)t.z | ((uint64_t)t.w << 32);
+      const uint64_t v0 = (uint64_t)vk.x | ((uint64_t)vk.y << 32), v1 = (uint64_t)vk.z | ((uint64_t)vk.w << 32);
+      const bool any = ((t0 & v0) | (t1 & v1)) != 0;
+      // has_new_bits' 2: a nonzero byte of the trace where the virgin byte is still 0xff
+      const bool two = ((nonzero_bytes8(t0) & ~nonzero_bytes8(~v0)) |
+                        (nonzero_bytes8(t1) & ~nonzero_bytes8(~v1))) != 0;
+      vk = make_uint4(vk.x & ~t.x, vk.y & ~t.y, vk.z & ~t.z, vk.w & ~t.w);
+      if (k == 0) v[0] = vk;
+      else if (k == 1) v[1] = vk;
+      else v[2] = vk;
+      const uint64_t b2 = __ballot(two), b1 = __ballot(any);
+      if ((b1 | b2) && lane == 0) atomicMax(&score[j], b2 ? 2u : 1u);
+    }
+  }
+  if (live)
+#pragma unroll
+    for (int k = 0; k < 3; k++) *(uint4 *)(a.vnext + (size_t)k * a.map_size + col) = v[k];
+  __syncthreads();  // every wave's scores are in score[]
+  if (threadIdx.x < n && score[threadIdx.x]) atomicMax(&a.hnb32[threadIdx.x], score[threadIdx.x]);
+  // hand-off to the last workgroup: every wave's atomics complete, then one release + ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (threadIdx.x < n) {
+    const uint32_t h = __hip_atomic_load(&a.hnb32[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.hnb_out) a.hnb_out[threadIdx.x] = (uint8_t)h;
+    __hip_atomic_store(&a.hnb32[threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.stats[0] = a.stats[1] = a.stats[2] = 0;  // no claim items, no fix path
+  }
 }
 
 __global__ __launch_bounds__(256) void k_or_reduce(uint8_t *out, const uint8_t *in, size_t r_lo,
@@ -2581,9 +2726,11 @@ struct kbz_ctx {
   uint64_t *items = nullptr;
   uint32_t item_cap = 0;
   uint32_t win_items = KBZ_WIN_ITEMS;  // claimed bytes per chunk x 1-KiB window: window item
+  bool small_ok = true;  // k_small for small AFL batches (tests: KBZ_DEBUG_NO_SMALL=1 disables)
   uint32_t *counters = nullptr;  // [0] items, [1] overflow, [2] resolve error, [3] fix list,
                                  // [4] bad rows, [6..7] clean flags of the saved rows,
-                                 // [8..10] the last finished batch's [0], [3], [4]
+                                 // [8..10] the last finished batch's [0], [3], [4],
+                                 // [12] k_small's workgroup ticket
   uint32_t *shard_last = nullptr;  // [2]
   // in-flight shard
   const uint8_t *cur_traces = nullptr;
@@ -2884,6 +3031,8 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   if (const char *cap = getenv("KBZ_DEBUG_ITEM_CAP")) c->item_cap = std::max(1, atoi(cap));
   // tests only: force window items everywhere (1) or never (a large value)
   if (const char *w = getenv("KBZ_DEBUG_WIN_ITEMS")) c->win_items = (uint32_t)std::max(1, atoi(w));
+  // tests only: small AFL batches through the general pipeline instead of k_small
+  if (const char *w = getenv("KBZ_DEBUG_NO_SMALL")) c->small_ok = atoi(w) == 0;
   bool ok = !dalloc(&c->V[0], 3 * M) && !dalloc(&c->V[1], 3 * M) && !dalloc(&c->last, 2) &&
             !dalloc(&c->chunk_or, c->max_chunks * nc * M) && !dalloc(&c->chunk_cls, c->max_chunks) &&
             !dalloc(&c->tflags, c->max_chunks * nc * c->nfw) &&
@@ -3296,6 +3445,24 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
 int kbz_triage_batch_device(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride,
                             const int8_t *outcome, uint8_t *hnb_out, uint32_t *h32_out,
                             uint64_t *x64_out, int want, void *stream) {
+  // AFL modes, no hash, at most 64 execs (the AFL plugin's per-exec flushes): one launch
+  if (c && c->small_ok && c->mode != KBZ_MODE_DYNAMORIO && n && n <= kSmallRows && c->stage == 0 &&
+      !h32_out && !(want & (KBZ_WANT_H32 | KBZ_WANT_X64))) {
+    if (check_rows(traces, stride, c->M)) return -1;
+    if (n > c->max_batch) return fail("n exceeds max_batch");
+    DevGuard g(c->device);
+    const int vn = c->vcur ^ 1;
+    SmallArgs a{traces, stride, (uint32_t)n, (uint32_t)c->M, outcome, c->V[c->vcur], c->V[vn],
+                c->hnb32, hnb_out, c->counters + 12, c->counters + 8};
+    const dim3 grid(cdiv(c->M / 16, 256));
+    if (c->mode == KBZ_MODE_AFL)
+      hipLaunchKernelGGL(k_small<KBZ_MODE_AFL>, grid, dim3(256), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(k_small<KBZ_MODE_AFL_CLASSIFY>, grid, dim3(256), 0, (hipStream_t)stream, a);
+    HIP_TRY(hipGetLastError());
+    c->vcur = vn;
+    return 0;
+  }
   if (kbz_shard_begin(c, traces, n, stride, outcome, h32_out, x64_out, want, stream)) return -1;
   if (kbz_shard_link(c, nullptr, nullptr, 1, nullptr, nullptr, stream)) return -1;
   if (kbz_shard_reduce(c, stream)) return -1;
@@ -3322,6 +3489,18 @@ int kbz_or_reduce(uint8_t *out, const uint8_t *in, size_t r_lo, size_t r_hi, siz
   return 0;
 }
 
+#ifdef KBZ_TAIL_STAMPS
+// diagnostic build only: k_scan's per-wave records {entry, prologue done, exit, counters}
+int kbz_debug_tail(unsigned long long *host_out, size_t count) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_kbz_tail),
+                              std::min<size_t>(count, (size_t)kTailRecs * 4) * 8));
+  void *sym = nullptr;
+  HIP_TRY(hipGetSymbolAddress(&sym, HIP_SYMBOL(g_kbz_tail)));
+  HIP_TRY(hipMemset(sym, 0, (size_t)kTailRecs * 4 * 8));
+  return 0;
+}
+#endif
 #ifdef KBZ_STAMPS
 // diagnostic build only: per (chunk, wave) cycles {compute, vmcnt wait, fill+prefetch, barrier}
 int kbz_debug_stamps(unsigned long long *host_out, size_t count) {

@@ -159,32 +159,29 @@ def merge_sharded(states, world, group=None, fold=None, out=None):
 
 # ---- unique crash/hang table across GPUs (BASELINE config 5) ----------------
 
-def dedup_sharded(table, keys, mask, rank, world, group=None):
+def dedup_sharded(table, keys, mask, rank, world, group=None, cap=None):
     """The reference's insert-if-absent set novelty (linux_ipt_instrumentation.c:412-424: new iff
     the key was absent; HASH_ADD keeps insertion order) over a batch sharded by contiguous trace
     index.  keys: this rank's [n_r, 2] int64 keys (e.g. {XXH64 of the transformed trace,
     outcome class}: triage.dedup_keys); mask: [n_r] bool/uint8, rows that take part (crash and
-    hang traces).  The masked keys of all ranks are all-gathered in rank order -- i.e. in global
-    trace order, with their global position implicit in that order -- and inserted as ONE
-    ordered batch into every rank's replica `table` (any object with UniqueSet.insert), so all
-    replicas stay identical and the first occurrence in global order is the new one.  Returns
-    this rank's is_new [n_r] uint8 (0 for masked-out rows)."""
+    hang traces).  Every rank's rows are all-gathered in rank order -- i.e. in global trace
+    order -- as ONE fixed-shape buffer of cap rows per rank {key, mask} (padding rows masked
+    out; cap = the largest shard, default n_r: equal shards), and inserted as one ordered, masked
+    batch into every rank's replica `table` (any object with UniqueSet.insert(keys, mask)), so
+    all replicas stay identical and the first occurrence in global order is the new one.  No
+    host synchronisation and no host-side concatenation: the masking happens in the insert.
+    Returns this rank's is_new [n_r] uint8 (0 for masked-out rows)."""
     dev = keys.device
-    m = mask.to(torch.bool)
-    sel = keys[m].contiguous()
-    if world > 1:
-        cnt = torch.tensor([sel.shape[0]], dtype=torch.int64, device=dev)
-        cnts = _all_gather(cnt, world, group).view(-1).tolist()
-        mx = max(cnts)
-        pad = torch.zeros((mx, 2), dtype=keys.dtype, device=dev)
-        pad[:sel.shape[0]] = sel
-        allk = _all_gather(pad, world, group)  # [world, mx, 2]
-        glob = torch.cat([allk[r, :cnts[r]] for r in range(world)]) if sum(cnts) else pad[:0]
-        off = sum(cnts[:rank])
-    else:
-        glob, off = sel, 0
-    isnew_all = table.insert(glob) if glob.shape[0] else torch.zeros(0, dtype=torch.uint8,
-                                                                     device=dev)
-    out = torch.zeros(keys.shape[0], dtype=torch.uint8, device=dev)
-    out[m] = isnew_all[off:off + sel.shape[0]].to(torch.uint8)
-    return out
+    n = keys.shape[0]
+    m8 = mask.to(torch.int64).view(-1, 1)
+    if world == 1:
+        return table.insert(keys, mask=mask.to(torch.uint8)).to(torch.uint8)
+    cap = n if cap is None else cap
+    if n > cap:
+        raise ValueError("dedup_sharded: shard larger than cap")
+    buf = torch.zeros((cap, 3), dtype=torch.int64, device=dev)
+    buf[:n, :2] = keys
+    buf[:n, 2:] = m8
+    allb = _all_gather(buf, world, group).view(world * cap, 3)
+    isnew = table.insert(allb[:, :2].contiguous(), mask=allb[:, 2].to(torch.uint8))
+    return isnew[rank * cap:rank * cap + n].to(torch.uint8)

@@ -33,10 +33,10 @@ _ref = None
 
 def build(force: bool = False) -> None:
     """Compile the restatement (and the reference oracle when /root/reference exists)."""
-    if force or not os.path.exists(LIB_PATH):
-        subprocess.check_call(["make", "-s", "-C", HERE, "libkbz_oracle.so"])
-    if os.path.isdir("/root/reference") and (force or not os.path.exists(REF_PATH)):
-        subprocess.check_call(["make", "-s", "-C", HERE, "ref"])
+    # make decides what is stale (sources, and the Makefile's flags for the reference build)
+    subprocess.check_call(["make", "-s", "-C", HERE, *(["-B"] if force else []), "libkbz_oracle.so"])
+    if os.path.isdir("/root/reference"):
+        subprocess.check_call(["make", "-s", "-C", HERE, *(["-B"] if force else []), "ref"])
 
 
 def _p(a):

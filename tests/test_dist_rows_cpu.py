@@ -41,10 +41,11 @@ class OrderedSetTable:
     def __init__(self):
         self.keys = {}
 
-    def insert(self, keys):
+    def insert(self, keys, mask=None):
         out = torch.zeros(keys.shape[0], dtype=torch.uint8)
+        m = [1] * keys.shape[0] if mask is None else mask.tolist()
         for j, (a, b) in enumerate(keys.tolist()):
-            if (a, b) not in self.keys:
+            if m[j] and (a, b) not in self.keys:
                 self.keys[(a, b)] = len(self.keys)
                 out[j] = 1
         return out
@@ -76,7 +77,8 @@ def _worker(rank, world, port, counts, q):
     for b in range(2):  # two batches: the replica carries over
         k, m = _keys(sum(counts), 20 + b)
         news.append(dedup_sharded(tab, torch.from_numpy(k[lo:lo + n].copy()),
-                                  torch.from_numpy(m[lo:lo + n].copy()), rank, world).numpy())
+                                  torch.from_numpy(m[lo:lo + n].copy()), rank, world,
+                                  cap=max(counts)).numpy())
     q.put((rank, merged.numpy(), news, list(tab.keys)))
     dist.destroy_process_group()
 

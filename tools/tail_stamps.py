@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""k_scan per-wave records of a KBZ_TAIL_STAMPS build (diagnostic only, never for results):
+config-2 fresh batches (bench.py's generator, DynamoRIO), then, per batch, the distribution of
+wave durations in k_scan, the prologue share, and the work of the slowest waves (chunks walked,
+inline claims, window items).
+usage: KBZ_HIP_LIB=build_variants/tailst/libkbz_hip.so python tools/tail_stamps.py [mode]"""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from killerbeez_amd import _lib, synth  # noqa: E402
+from killerbeez_amd.triage import MODES, WANT_H32, TriageContext  # noqa: E402
+
+mode_name = sys.argv[1] if len(sys.argv) > 1 else "dynamorio"
+B, M = 65536, 65536
+L = _lib.lib()
+assert L.kbz_build_flags() != b"", "needs the KBZ_TAIL_STAMPS variant (KBZ_HIP_LIB=...)"
+f = L.kbz_debug_tail
+f.restype = C.c_int
+f.argtypes = [C.c_void_p, C.c_size_t]
+NREC = 1 << 16
+buf = np.zeros(NREC * 4, np.uint64)
+dev = torch.device("cuda:0")
+mode = MODES[mode_name]
+want = WANT_H32 if mode == MODES["dynamorio"] else 0
+pool = [synth.sparse_torch(B, M, seed=1 + 7919 * p, device=dev, hot_seed=1) for p in range(8)]
+out = {"hnb": torch.empty(B, dtype=torch.uint8, device=dev)}
+res = []
+with TriageContext(M, mode, B) as ctx:
+    for i, (t, oc) in enumerate(pool):
+        f(buf.ctypes.data, 0)  # clears the records
+        ctx.triage(t, oc, want, out=out)
+        torch.cuda.synchronize()
+        ctx.sync()
+        assert f(buf.ctypes.data, NREC * 4) == 0
+        r = buf.reshape(NREC, 4)
+        live = r[r[:, 0] != 0]
+        t0 = live[:, 0].astype(np.int64)
+        t1 = live[:, 1].astype(np.int64)
+        t2 = live[:, 2].astype(np.int64)
+        cnt = live[:, 3]
+        walk = (cnt >> 48) & 0xFFFF
+        claims = (cnt >> 32) & 0xFFFF
+        win = cnt & 0xFFFF
+        base = t0.min()
+        dur = (t2 - t0) / 100.0  # us (100 MHz)
+        order = np.argsort(-dur)
+        rec = {
+            "batch": i, "waves": int(len(live)),
+            "span_us": round((t2.max() - base) / 100.0, 2),
+            "start_skew_us": round((t0.max() - base) / 100.0, 2),
+            "walking_waves": int((walk > 0).sum()),
+            "dur_us_p50_p90_max": [round(float(np.percentile(dur, q)), 2) for q in (50, 90, 100)],
+            "prologue_us_p50_max": [round(float(np.percentile((t1 - t0) / 100.0, q)), 2)
+                                    for q in (50, 100)],
+            "walk_total": int(walk.sum()), "claims_total": int(claims.sum()),
+            "windows_total": int(win.sum()),
+            "slowest": [{"dur_us": round(float(dur[j]), 2), "start_us": round((t0[j] - base) / 100.0, 2),
+                         "walk": int(walk[j]), "claims": int(claims[j]), "win": int(win[j])}
+                        for j in order[:6]],
+        }
+        res.append(rec)
+        print(json.dumps(rec), flush=True)
