@@ -344,6 +344,7 @@ struct Pass1Args {
   const uint8_t *vcur;  // [3][map_size] virgin maps at batch entry
   uint64_t *tflags;     // [chunks][nclass][nfw]: bit t%64 of word t/64 = tile t of chunk_or stored
   uint32_t nfw;         // flag words per (chunk, class) = ceil(tiles / 64)
+  uint8_t *hnb_clear;   // [n] or null: zeroed here (the fused tail writes only rows it scores)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -695,6 +696,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
     // lane 0 has no predecessor in the wave: its value is a placeholder (k_skip compares a chunk's
     // row 0 with the previous row itself, and only when their hashes are equal)
     if (MODE == KBZ_MODE_DYNAMORIO && valid) a.neq[row0 + lane] = neq != 0;
+    if (a.hnb_clear && valid) a.hnb_clear[row0 + lane] = 0;
   }
 }
 
@@ -861,6 +863,7 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
     if (isL && valid) {
       const uint32_t h32 = h32_final(h);
       a.h32[row0 + lane] = h32;
+      if (a.hnb_clear) a.hnb_clear[row0 + lane] = 0;
       if (X64 && a.x64) {
         uint64_t xh = rotl64(x0, 1) + rotl64(x1, 7) + rotl64(x2, 12) + rotl64(x3, 18);
         xh = xx_merge(xh, x0);
@@ -1299,6 +1302,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
     }
   }
   drain_asm_loads(R);
+  if (a.hnb_clear && wave == 0 && lane < nrows) a.hnb_clear[row0 + lane] = 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1449,6 +1453,7 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
     if (lane < nrows) {
       const uint32_t h32 = h32_final(h);
       a.h32[row0 + lane] = h32;
+      if (a.hnb_clear) a.hnb_clear[row0 + lane] = 0;
       if (X64 && a.x64) {
         uint64_t xh = rotl64(x0, 1) + rotl64(x1, 7) + rotl64(x2, 12) + rotl64(x3, 18);
         xh = xx_merge(xh, x0);
@@ -1657,16 +1662,55 @@ __device__ __forceinline__ int rows_differ(const uint8_t *x, const uint8_t *y, c
 // last-hash pair (shard_last[1], bit 0 = non-empty) gets bit 1 = "has a bad row j >= 1" and
 // bit 2 = "has a non-skipped row j >= 1": a shard with bit 2 and without bit 1 ends in a clean
 // row (its last row's chain of links starts at a row that was applied), whatever its row 0 is.
+// Predecessor of the shard's row 0 (kbz_shard_link): unknown, the context's saved row (the
+// previous batch's last, clean iff *ok), or another shard's last row (clean iff its pair's
+// flags say so, see k_skip).
+enum { PRED_UNKNOWN = 0, PRED_SAVED = 1, PRED_PAIR = 2 };
+__device__ __forceinline__ bool pair_clean(uint32_t f) { return !(f & 2u) && (f & 4u); }
+
+// The fused tail's extra k_skip roles (one-shard batches, kbz_triage_batch_device): the block
+// after the chunk-start blocks does k_chain's row-0 test against the saved row (bad0 -> a
+// device word the tail reads), the blocks after it copy the batch's last row into the context
+// (the next batch's row-0 predecessor).  Null row0_hp: the sharded protocol (k_chain does both).
+struct SkipExtra {
+  const uint32_t *row0_hp;  // the context's last hash (row 0's predecessor hash)
+  int pred_saved;           // the saved row is valid ...
+  const uint32_t *pred_ok;  // ... and clean iff *pred_ok
+  const uint8_t *prow;      // the saved row
+  uint32_t *bad0;           // out: row 0 is skipped and differs / has an unknown predecessor
+  const uint8_t *copy_src;  // the batch's last row -> copy_dst (map_size bytes), or null
+  uint8_t *copy_dst;
+  uint32_t copy_blocks;
+};
 __global__ void k_skip(const uint32_t *h32, uint8_t *neq, uint32_t n, uint8_t *skip,
                        uint32_t *flags, uint32_t *fix_list, uint32_t *fix_cnt, uint32_t *bad_list,
                        uint32_t *bad_cnt, uint32_t *shard_last, const uint8_t *traces,
                        size_t stride, const uint8_t *ignore, uint32_t map_size,
-                       uint32_t row_blocks) {
+                       uint32_t row_blocks, SkipExtra x) {
   auto bad_row = [&](uint32_t j) {
     const uint32_t c = j / kChunk;
     if (atomicExch(&flags[c], 1u) == 0u) fix_list[atomicAdd(fix_cnt, 1u)] = c;
     bad_list[atomicAdd(bad_cnt, 1u)] = j;
   };
+  const uint32_t cs_end = row_blocks + (n > kChunk ? (n - 1) / kChunk : 0);
+  if (blockIdx.x >= cs_end) {  // fused tail only: row 0, then the copy of the last row
+    if (blockIdx.x == cs_end) {
+      const bool sk0 = h32[0] == *x.row0_hp;
+      const bool known = x.pred_saved && *x.pred_ok != 0;
+      const int diff = (sk0 && known) ? rows_differ(traces, x.prow, ignore, map_size) : 0;
+      if (threadIdx.x == 0) {
+        skip[0] = sk0;
+        *x.bad0 = sk0 && (!known || diff);
+      }
+      return;
+    }
+    const uint32_t cb = blockIdx.x - cs_end - 1;
+    if (x.copy_src)
+      for (uint32_t i = (cb * blockDim.x + threadIdx.x) * 16; i < map_size;
+           i += x.copy_blocks * blockDim.x * 16)
+        *(uint4 *)(x.copy_dst + i) = *(const uint4 *)(x.copy_src + i);
+    return;
+  }
   if (blockIdx.x >= row_blocks) {  // chunk start j = 64 c, c >= 1
     const uint32_t j = (blockIdx.x - row_blocks + 1) * kChunk;
     if (j >= n || h32[j] != h32[j - 1]) return;  // block-uniform
@@ -1700,11 +1744,30 @@ __global__ void k_skip(const uint32_t *h32, uint8_t *neq, uint32_t n, uint8_t *s
     atomicOr(&shard_last[1], want);
 }
 
-// Predecessor of the shard's row 0 (kbz_shard_link): unknown, the context's saved row (the
-// previous batch's last, clean iff *ok), or another shard's last row (clean iff its pair's
-// flags say so, see k_skip).
-enum { PRED_UNKNOWN = 0, PRED_SAVED = 1, PRED_PAIR = 2 };
-__device__ __forceinline__ bool pair_clean(uint32_t f) { return !(f & 2u) && (f & 4u); }
+// One wave per bad row (row 0 included when bad0): follow its chain of link rows (skipped and
+// equal to their predecessor), 64 rows per step, and list every chunk the chain enters (the bad
+// row's own chunk is listed already by k_skip; row 0's is listed here).
+__device__ __forceinline__ void chain_walks(uint32_t n, const uint8_t *skip, const uint8_t *neq,
+                            const uint32_t *bad_list, uint32_t nbad, bool bad0, uint32_t *flags,
+                            uint32_t *fix_list, uint32_t *fix_cnt) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  auto list = [&](uint32_t c) {
+    if (atomicExch(&flags[c], 1u) == 0u) fix_list[atomicAdd(fix_cnt, 1u)] = c;
+  };
+  const uint32_t cnt = nbad + (bad0 ? 1u : 0u);
+  for (uint32_t i = wave; i < cnt; i += blockDim.x / 64) {
+    const uint32_t b = (bad0 && i == cnt - 1) ? 0u : bad_list[i];
+    if (b == 0 && lane == 0) list(0);
+    for (uint32_t j0 = b + 1; j0 < n; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      const bool lk = j < n && skip[j] && !neq[j];
+      const uint64_t stop = __ballot(!lk);
+      const uint32_t len = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;  // links from j0 on
+      if (lane < len && (j % kChunk) == 0) list(j / kChunk);  // chunk starts on the chain
+      if (len < 64) break;
+    }
+  }
+}
 
 struct ChainArgs {
   uint32_t n;
@@ -1763,22 +1826,9 @@ __global__ __launch_bounds__(256) void k_chain(ChainArgs a) {
       *a.saved_ok = a.copy_src ? pair_clean(a.global_last[1]) : 0u;
     }
   }
-  auto list = [&](uint32_t c) {
-    if (atomicExch(&a.flags[c], 1u) == 0u) a.fix_list[atomicAdd(a.fix_cnt, 1u)] = c;
-  };
-  const uint32_t cnt = *a.bad_cnt + (bad0 ? 1u : 0u);
-  for (uint32_t i = wave; i < cnt; i += blockDim.x / 64) {
-    const uint32_t b = (bad0 && i == cnt - 1) ? 0u : a.bad_list[i];
-    if (b == 0 && lane == 0) list(0);
-    for (uint32_t j0 = b + 1; j0 < n; j0 += 64) {
-      const uint32_t j = j0 + lane;
-      const bool lk = j < n && a.skip[j] && !a.neq[j];
-      const uint64_t stop = __ballot(!lk);
-      const uint32_t len = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;  // links from j0 on
-      if (lane < len && (j % kChunk) == 0) list(j / kChunk);  // chunk starts on the chain
-      if (len < 64) break;
-    }
-  }
+  (void)lane;
+  (void)wave;
+  chain_walks(n, a.skip, a.neq, a.bad_list, *a.bad_cnt, bad0, a.flags, a.fix_list, a.fix_cnt);
 }
 
 // DynamoRIO fix path of the skip rule, for k_total: chunks listed by k_skip hold a skipped trace
@@ -1807,7 +1857,7 @@ __device__ __forceinline__ bool tile_stored(const uint64_t *tflags, uint32_t nfw
   const uint32_t t = col / kTileW;
   return (tflags[((size_t)c * nclass + k) * nfw + (t >> 6)] >> (t & 63)) & 1;
 }
-__device__ void fix_column(const FixArgs &f, uint32_t map_size, uint32_t col, uint8_t *segor) {
+__device__ __forceinline__ void fix_column(const FixArgs &f, uint32_t map_size, uint32_t col, uint8_t *segor) {
   const uint32_t cnt = min(*f.fix_cnt, f.nchunks);
   for (uint32_t i = 0; i < cnt; i++) {
     const uint32_t chunk = f.fix_list[i];
@@ -1860,11 +1910,41 @@ __global__ __launch_bounds__(256) void k_total(uint8_t *segor, uint32_t nseg, in
                       // batches (step 0.77-0.78 vs 0.80-0.81 ms, profiles/r02_v10/ab_scan_ilp.txt)
 #define KBZ_SCAN_ILP 8
 #endif
-// item: [7:0] new bits, [8] score-2 candidate, [10:9] class, [34:11] column, [63:35] chunk
+// item: [7:0] new bits, [8] score-2 candidate, [10:9] class, [34:11] column, [59:35] chunk,
+// [63] present (never 0: the fused tail tells a written slot from a reserved one by it; every
+// resolver zeroes the slots it consumed, so the list is all-zero between batches)
+constexpr uint64_t kItemPresent = 1ull << 63;
 __device__ __forceinline__ uint64_t pack_item(uint32_t chunk, int k, uint32_t col, uint32_t nb,
                                               bool f2) {
-  return ((uint64_t)chunk << 35) | ((uint64_t)col << 11) | ((uint64_t)k << 9) |
+  return kItemPresent | ((uint64_t)chunk << 35) | ((uint64_t)col << 11) | ((uint64_t)k << 9) |
          ((uint64_t)f2 << 8) | nb;
+}
+__device__ __forceinline__ uint32_t item_chunk(uint64_t item) { return (uint32_t)((item >> 35) & 0x1FFFFFFu); }
+// Hand-off stores and loads between workgroups of one launch (the fused tail): agent-scope
+// relaxed atomics, i.e. sc1 accesses performed at the coherence point, so another XCD's reader
+// sees them without cache maintenance (MI355X_MICROARCH.md, hand-off rules).
+__device__ __forceinline__ void st_sc1(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// A claim's score for trace `row` (has_new_bits' 1 or 2, the maximum over its claims).  With a
+// touched list (the fused tail) the first scorer of a row also lists it, so the tail's last
+// workgroup copies only scored rows into hnb_out (pass 1 zeroed the others).
+__device__ __forceinline__ void score_row(uint32_t *hnb32, uint32_t *touched, uint32_t *tcount,
+                                          uint64_t row, uint32_t v) {
+  if (!touched) {
+    atomicMax(&hnb32[row], v);
+    return;
+  }
+  if (atomicMax(&hnb32[row], v) == 0u) st_sc1(&touched[atomicAdd(tcount, 1u)], (uint32_t)row);
 }
 
 // Append this lane's claim items (one per nonzero byte of nb) with ONE atomic per wave:
@@ -1891,12 +1971,14 @@ struct ItemStage {
 __device__ __forceinline__ void flush_items(ItemStage &st, uint64_t *items, uint32_t cap,
                                             uint32_t *counters) {
   if (!st.n) return;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's staged writes are done
+  // the wave's staged LDS writes and its window-prefix stores (emit_items_wave) are done: an
+  // item never becomes visible before the data it names
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   uint32_t base = 0;
   if ((threadIdx.x & 63) == 0) base = atomicAdd(&counters[0], st.n);
   base = __shfl(base, 0);
   for (uint32_t i = threadIdx.x & 63; i < st.n; i += 64) {
-    if (base + i < cap) items[base + i] = st.buf[i];
+    if (base + i < cap) st_sc1(&items[base + i], st.buf[i]);
     else atomicOr(&counters[1], 1u);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the area is reused
@@ -1922,7 +2004,10 @@ __device__ __forceinline__ void emit_items_wave(uint32_t chunk, int k, uint32_t 
     // window item (new bits field 0): the wave's 1-KiB column window of this chunk.  The running
     // OR before this chunk replaces the chunk's (consumed) column OR in chunk_or, and k_resolve
     // re-derives the claims row by row in order: new bits of row r = t_r & V & ~(prev | rows < r)
-    if (live) *(uint4 *)win_prev = prev;
+    if (live) {  // read by whichever wave resolves the item (maybe another workgroup)
+      st_sc1((uint64_t *)win_prev, (uint64_t)prev.x | ((uint64_t)prev.y << 32));
+      st_sc1((uint64_t *)win_prev + 1, (uint64_t)prev.z | ((uint64_t)prev.w << 32));
+    }
     const uint32_t wcol = __shfl(col, 0);
     if (st.n + 1 > kWaveItems) flush_items(st, items, cap, counters);
     if ((threadIdx.x & 63) == 0) st.buf[st.n] = pack_item(chunk, k, wcol, 0u, false);
@@ -1946,7 +2031,7 @@ __device__ __forceinline__ void emit_items_wave(uint32_t chunk, int k, uint32_t 
       const bool f2 = ((vv[i] >> (8 * b)) & 0xff) == 0xff && ((pv[i] >> (8 * b)) & 0xff) == 0;
       const uint64_t it = pack_item(chunk, k, col + 4 * i + b, x, f2);
       if (staged) st.buf[base] = it;
-      else if (base < cap) items[base] = it;
+      else if (base < cap) st_sc1(&items[base], it);
       else atomicOr(&counters[1], 1u);
       base++;
     }
@@ -1965,6 +2050,8 @@ struct ClaimArgs {  // what k_scan needs to resolve claims inline (k_resolve's i
   const uint8_t *skip;
   uint32_t *hnb32;
   uint32_t *err;
+  uint32_t *touched;  // fused tail: rows scored so far (null: the staged pipeline's k_pack)
+  uint32_t *tcount;
 };
 __device__ __forceinline__ uint32_t pick4(uint4 v, int i) {  // i wave-uniform
   return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
@@ -1980,7 +2067,7 @@ struct ClaimQ {
   uint4 *q;  // this wave's kClaimQ entries in LDS: {chunk, column, new bits | f2 << 8, 0}
   int m;     // wave-uniform fill
 };
-__device__ void claims_flush(const ClaimArgs &ca, int k, ClaimQ &cq) {
+__device__ __forceinline__ void claims_flush(const ClaimArgs &ca, int k, ClaimQ &cq) {
   if (!cq.m) return;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // lane 0's entries are written
   const int lane = threadIdx.x & 63;
@@ -2016,14 +2103,14 @@ __device__ void claims_flush(const ClaimArgs &ca, int k, ClaimQ &cq) {
     }
     if ((claimers >> lane) & 1) {
       const bool two = (e[j].z >> 8) && first_nz && (lane == __builtin_ctzll(first_nz));
-      atomicMax(&ca.hnb32[row], two ? 2u : 1u);
+      score_row(ca.hnb32, ca.touched, ca.tcount, row, two ? 2u : 1u);
     }
   }
   asm volatile("" ::: "memory");
   cq.m = 0;
 }
 // Queue the claimed bytes of this wave's window of chunk `chunk` (flushing every kClaimQ).
-__device__ void claims_enqueue(const ClaimArgs &ca, int k, ClaimQ &cq, uint32_t chunk,
+__device__ __forceinline__ void claims_enqueue(const ClaimArgs &ca, int k, ClaimQ &cq, uint32_t chunk,
                                uint32_t col, uint4 nb, uint4 vir, uint4 prev) {
   const int lane = threadIdx.x & 63;
   uint32_t rem = 0;  // this lane's claimed bytes, bit i = byte i of its 16
@@ -2081,6 +2168,7 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
   // no per-lane early return: every lane of a wave takes part in the item-allocation prefix
   KBZ_TAIL_DECL;
   const uint32_t tail_id = ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6);
+  (void)tail_id;
   const uint32_t col0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
   const bool live = col0 < map_size;
   const uint32_t col = live ? col0 : 0;
@@ -2201,28 +2289,42 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
 // `acc`: row r claims t_r & V & ~(prev | acc) (has_new_bits, afl_instrumentation.c:600-662, over
 // the window), and scores 2 if it is the first row with a nonzero byte where V is 0xff and prev
 // is 0 (:644-651).  Rows are loaded 8 at a time (1 KiB per row, coalesced).
-__device__ __forceinline__ void resolve_window(const uint8_t *traces, size_t stride, uint32_t n,
-                                               int mode, const int8_t *outcome,
-                                               const uint8_t *skip, uint32_t chunk, int k,
-                                               uint32_t wcol, const uint8_t *win_prev,
-                                               const uint8_t *vcur, const uint8_t *ignore,
-                                               uint32_t map_size, uint32_t *hnb32,
-                                               uint32_t *err) {
+struct ResolveArgs {  // what resolving a claim item needs (k_resolve, the fused tail)
+  const uint8_t *traces;
+  size_t stride;
+  uint32_t n;
+  int mode;
+  const int8_t *outcome;
+  const uint8_t *skip;
+  uint32_t *hnb32;
+  uint32_t *err;
+  const uint8_t *chunk_or;
+  int nclass;
+  uint32_t map_size;
+  const uint8_t *vcur;
+  const uint8_t *ignore;
+  uint32_t *touched;  // see ClaimArgs
+  uint32_t *tcount;
+};
+__device__ __forceinline__ void resolve_window(const ResolveArgs &r, uint32_t chunk, int k,
+                                               uint32_t wcol, const uint8_t *win_prev) {
   const int lane = threadIdx.x & 63;
   const uint64_t row0 = (uint64_t)chunk * kChunk;
   const uint64_t rl = row0 + lane;
-  bool ok = rl < n;
-  if (ok && outcome) ok = class_of(mode, outcome[rl]) == k;
-  if (ok && skip) ok = !skip[rl];
+  bool ok = rl < r.n;
+  if (ok && r.outcome) ok = class_of(r.mode, r.outcome[rl]) == k;
+  if (ok && r.skip) ok = !r.skip[rl];
   uint64_t rows = __ballot(ok);
   const uint32_t col = wcol + 16 * lane;
-  const bool live = col < map_size;
+  const bool live = col < r.map_size;
   const uint32_t cl = live ? col : wcol;
-  const uint4 prev = *(const uint4 *)(win_prev + (cl - wcol));  // k_scan's running OR
-  const uint4 vir = *(const uint4 *)(vcur + (size_t)k * map_size + cl);
+  // k_scan's running OR (maybe stored by another workgroup of the fused tail: sc1 loads)
+  const uint64_t *wp = (const uint64_t *)(win_prev + (cl - wcol));
+  uint64_t pa0 = ld_sc1(wp), pa1 = ld_sc1(wp + 1);
+  const uint4 vir = *(const uint4 *)(r.vcur + (size_t)k * r.map_size + cl);
   uint64_t rel0 = ~0ull, rel1 = ~0ull;
-  if (ignore) {
-    const uint4 ig = *(const uint4 *)(ignore + cl);
+  if (r.ignore) {
+    const uint4 ig = *(const uint4 *)(r.ignore + cl);
     rel0 = ~nonzero_bytes8((uint64_t)ig.x | ((uint64_t)ig.y << 32));
     rel1 = ~nonzero_bytes8((uint64_t)ig.z | ((uint64_t)ig.w << 32));
   }
@@ -2231,9 +2333,7 @@ __device__ __forceinline__ void resolve_window(const uint8_t *traces, size_t str
   if (!live) vr0 = vr1 = 0;
   // bytes with V == 0xff (examined): a 2 is possible there while prev | acc is still 0
   const uint64_t ff0 = ~nonzero_bytes8(~vr0), ff1 = ~nonzero_bytes8(~vr1);
-  uint64_t pa0 = (uint64_t)prev.x | ((uint64_t)prev.y << 32);
-  uint64_t pa1 = (uint64_t)prev.z | ((uint64_t)prev.w << 32);
-  const int xf = class_xf(mode, k);
+  const int xf = class_xf(r.mode, k);
   bool claimed = false;
   while (rows) {
     int rr[8];
@@ -2242,8 +2342,8 @@ __device__ __forceinline__ void resolve_window(const uint8_t *traces, size_t str
     for (int u = 0; u < 8; u++) {  // up to 8 rows' loads in flight
       rr[u] = rows ? __builtin_ctzll(rows) : -1;
       rows &= rows - 1;
-      const uint64_t r = row0 + (rr[u] >= 0 ? rr[u] : 0);
-      v[u] = *(const uint4 *)(traces + r * stride + cl);
+      const uint64_t rw = row0 + (rr[u] >= 0 ? rr[u] : 0);
+      v[u] = *(const uint4 *)(r.traces + rw * r.stride + cl);
     }
 #pragma unroll
     for (int u = 0; u < 8; u++) {
@@ -2258,60 +2358,61 @@ __device__ __forceinline__ void resolve_window(const uint8_t *traces, size_t str
       const uint32_t sc = __ballot(two) ? 2u : __ballot(nw) ? 1u : 0u;
       if (sc) {
         claimed = true;
-        if (lane == 0) atomicMax(&hnb32[row0 + rr[u]], sc);
+        if (lane == 0) score_row(r.hnb32, r.touched, r.tcount, row0 + rr[u], sc);
       }
     }
   }
-  if (!claimed && lane == 0) atomicOr(err, 2u);  // k_scan saw new bits here: inconsistent
+  if (!claimed && lane == 0) atomicOr(r.err, 2u);  // k_scan saw new bits here: inconsistent
 }
 
-__global__ __launch_bounds__(256) void k_resolve(const uint8_t *traces, size_t stride, uint32_t n,
-                                                  int mode, const int8_t *outcome,
-                                                  const uint8_t *skip, const uint64_t *items,
-                                                  const uint32_t *counters, uint32_t cap,
-                                                  uint32_t *hnb32, uint32_t *err,
-                                                  const uint8_t *chunk_or, int nclass,
-                                                  uint32_t map_size, const uint8_t *vcur,
-                                                  const uint8_t *ignore) {
+// One claim item (wave-uniform): a window item (new bits field 0) or one claimed byte of one
+// chunk -- per new bit, the first trace of the chunk (class k, not skipped) holding it scores 1,
+// or 2 if the byte was all-virgin and it is the chunk's first trace with a nonzero byte there.
+__device__ __forceinline__ void resolve_item(const ResolveArgs &r, uint64_t item) {
   const int lane = threadIdx.x & 63;
+  const uint32_t nb = item & 0xff;
+  const bool f2 = (item >> 8) & 1;
+  const int k = (item >> 9) & 3;
+  const uint32_t col = (item >> 11) & 0xffffff;
+  const uint32_t chunk = item_chunk(item);
+  if (nb == 0) {  // window item
+    resolve_window(r, chunk, k, col,
+                   r.chunk_or + ((size_t)chunk * r.nclass + k) * r.map_size + col);
+    return;
+  }
+  const uint64_t row = (uint64_t)chunk * kChunk + lane;
+  const uint64_t rc = min(row, (uint64_t)r.n - 1);  // independent loads, one round trip
+  const int oc = r.outcome ? r.outcome[rc] : KBZ_FUZZ_NONE;
+  const uint8_t sk = r.skip ? r.skip[rc] : 0;
+  const uint32_t raw = r.traces[rc * r.stride + col];
+  const bool ok = row < r.n && class_of(r.mode, oc) == k && !sk;
+  const uint32_t tb = ok ? byte_xform(raw, class_xf(r.mode, k)) : 0u;
+  const uint64_t first_nz = __ballot(tb != 0);
+  uint64_t claimers = 0;
+  for (int b = 0; b < 8; b++) {
+    if ((nb >> b) & 1) {
+      const uint64_t m = __ballot((tb >> b) & 1);
+      if (!m) {
+        if (lane == 0) atomicOr(r.err, 2u);
+      }
+      claimers |= m & (0 - m);
+    }
+  }
+  if ((claimers >> lane) & 1) {
+    const bool two = f2 && first_nz && (lane == __builtin_ctzll(first_nz));
+    score_row(r.hnb32, r.touched, r.tcount, row, two ? 2u : 1u);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_resolve(ResolveArgs r, uint64_t *items,
+                                                  const uint32_t *counters, uint32_t cap) {
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   const uint32_t cnt = min(counters[0], cap);
   for (uint32_t it = wave; it < cnt; it += nwaves) {
     const uint64_t item = items[it];
-    const uint32_t nb = item & 0xff;
-    const bool f2 = (item >> 8) & 1;
-    const int k = (item >> 9) & 3;
-    const uint32_t col = (item >> 11) & 0xffffff;
-    const uint32_t chunk = (uint32_t)(item >> 35);
-    if (nb == 0) {  // window item (wave-uniform)
-      resolve_window(traces, stride, n, mode, outcome, skip, chunk, k, col,
-                     chunk_or + ((size_t)chunk * nclass + k) * map_size + col, vcur, ignore,
-                     map_size, hnb32, err);
-      continue;
-    }
-    const uint64_t row = (uint64_t)chunk * kChunk + lane;
-    const uint64_t rc = min(row, (uint64_t)n - 1);  // independent loads, one round trip
-    const int oc = outcome ? outcome[rc] : KBZ_FUZZ_NONE;
-    const uint8_t sk = skip ? skip[rc] : 0;
-    const uint32_t raw = traces[rc * stride + col];
-    const bool ok = row < n && class_of(mode, oc) == k && !sk;
-    const uint32_t tb = ok ? byte_xform(raw, class_xf(mode, k)) : 0u;
-    const uint64_t first_nz = __ballot(tb != 0);
-    uint64_t claimers = 0;
-    for (int b = 0; b < 8; b++) {
-      if ((nb >> b) & 1) {
-        const uint64_t m = __ballot((tb >> b) & 1);
-        if (!m) {
-          if (lane == 0) atomicOr(err, 2u);
-        }
-        claimers |= m & (0 - m);
-      }
-    }
-    if ((claimers >> lane) & 1) {
-      const bool two = f2 && first_nz && (lane == __builtin_ctzll(first_nz));
-      atomicMax(&hnb32[row], two ? 2u : 1u);
-    }
+    resolve_item(r, item);
+    if ((threadIdx.x & 63) == 0) items[it] = 0;  // the list is all-zero between batches
   }
 }
 
@@ -2341,6 +2442,313 @@ __global__ void k_pack(uint32_t *hnb32, const uint32_t *h32, uint32_t n, uint8_t
   if (hnb_out) hnb_out[j] = (uint8_t)hnb32[j];
   if (h32_out) h32_out[j] = h32[j];
   hnb32[j] = 0;  // ready for the next batch
+}
+
+// ---------------------------------------------------------------------------------------------
+// The fused tail of a one-shard batch (kbz_triage_batch_device): everything after pass 1 (and,
+// in DynamoRIO mode, after k_skip with its row-0 / saved-row roles) in ONE launch, in place of
+// k_chain, k_total, k_scan, k_resolve and k_pack.  Grid (column groups of 4 KiB, segments,
+// classes) as k_scan; a workgroup:
+//   1. DynamoRIO, only when k_skip found bad rows (hash collisions): workgroup 0 finishes
+//      k_chain's part (the chain walks), the segment-0 workgroup of each column group runs
+//      k_total's fix for its columns, the others wait for it (flags; every wait is on a
+//      workgroup of lower linear index, which was dispatched first: no deadlock at any grid size);
+//   2. k_scan's walk, with the segment prefixes taken from the segment ORs themselves (all 32
+//      loads in one round trip) instead of k_total's output; segment 0 writes V' = V & ~total;
+//   3. resolves the window items appended so far (claims it with a CAS on the taken counter);
+//   4. takes a ticket; the LAST workgroup resolves the items nobody took, copies the scored rows
+//      (a touched list: the first scorer of each row appends it) into hnb_out -- pass 1 zeroed
+//      the others -- and re-arms the per-batch state.
+// It also zeroes the other segment-OR buffer for the next batch (segor is double-buffered).
+// Hand-offs between workgroups use agent-scope atomics or sc1 stores/loads (score_row, st_sc1,
+// ld_sc1); the rare fix path publishes plain stores with release / acquire fences.
+// ---------------------------------------------------------------------------------------------
+constexpr int kTailFixDone = 16;  // tail words: [0] ticket [1] taken [2] touched [3] walks done
+                                  // [4] bad0 (k_skip) [5] fixing [16 + bx] column group bx fixed
+constexpr uint32_t kSpinMax = 1u << 22;
+__device__ __forceinline__ bool spin_until(const uint32_t *p, uint32_t want) {
+  for (uint32_t it = 0; it < kSpinMax; it++) {
+    if (ld_sc1(p) == want) return true;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
+struct TailArgs {
+  ClaimArgs ca;         // traces, stride, n, mode, outcome, skip, hnb32, err, touched, tcount
+  ResolveArgs ra;
+  FixArgs fx;           // DynamoRIO fix path (fx.fix_cnt = counters + 3)
+  uint8_t *chunk_or;
+  const uint8_t *chunk_cls;
+  uint32_t nchunks, seg_len, nseg;
+  int nclass;
+  uint32_t map_size;
+  uint8_t *segor;       // this batch's segment ORs
+  uint8_t *segor_next;  // the other buffer: zeroed for the next batch
+  const uint8_t *vcur;
+  uint8_t *vnext;
+  const uint8_t *ignore;
+  uint64_t *items;
+  uint32_t cap;
+  uint32_t *counters;
+  const uint64_t *tflags;
+  uint32_t nfw;
+  const uint32_t *listed;  // DynamoRIO: fix-list flags
+  uint32_t win_items;
+  uint8_t *hnb_out;
+  uint32_t *tail;
+  uint32_t *err_out;       // host-mapped copy of counters[1..2]
+  uint32_t *shard_last;
+  // DynamoRIO chain bookkeeping of k_chain (one shard)
+  const uint8_t *neq;
+  const uint32_t *bad_list;
+  const uint32_t *ctx_last;
+  uint32_t *next_last;
+  uint32_t *saved_ok;
+  uint32_t *flags_w, *fix_list_w, *fix_cnt_w;  // the walks' fix list (DynamoRIO)
+};
+__global__ __launch_bounds__(256) void k_tail(TailArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t bx = blockIdx.x, s = blockIdx.y;
+  const int k = blockIdx.z;
+  const uint32_t M = a.map_size;
+  const bool dr = a.ca.mode == KBZ_MODE_DYNAMORIO;
+  const bool wg0 = bx == 0 && s == 0 && k == 0;
+  const uint32_t col0 = (bx * blockDim.x + threadIdx.x) * 16;
+  const bool live = col0 < M;
+  const uint32_t col = live ? col0 : 0;
+  const size_t kc = (size_t)k * M + col;
+  __shared__ int sh_flag;
+  // the next batch's segment ORs start at zero (every segment of this column slice and class)
+  if (live)
+    for (uint32_t ss = s; ss < kMaxSeg; ss += a.nseg)
+      *(uint4 *)(a.segor_next + ((size_t)ss * a.nclass + k) * M + col) = make_uint4(0, 0, 0, 0);
+  // ---- 1. DynamoRIO chain / fix path -------------------------------------------------------
+  const uint32_t nbad = dr ? a.counters[4] : 0u, bad0 = dr ? a.tail[4] : 0u;
+  if (dr && wg0 && threadIdx.x == 0) {  // k_chain's bookkeeping for a one-shard batch
+    const uint32_t f = a.shard_last[1];
+    *a.next_last = f ? a.shard_last[0] : *a.ctx_last;
+    *a.saved_ok = (nbad == 0) && ((f & 4u) || !bad0);
+  }
+  bool fixing = false;
+  if (nbad + bad0) {  // block-uniform; rare (hash collisions)
+    if (wg0) {
+      chain_walks(a.ca.n, a.ca.skip, a.neq, a.bad_list, nbad, bad0 != 0, a.flags_w,
+                  a.fix_list_w, a.fix_cnt_w);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st_sc1(&a.tail[5], ld_sc1(a.fx.fix_cnt) != 0 ? 1u : 0u);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st_sc1(&a.tail[3], 1u);
+      }
+    }
+    if (threadIdx.x == 0) {
+      if (!spin_until(&a.tail[3], 1u)) atomicOr(a.ca.err, 4u);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      sh_flag = (int)ld_sc1(&a.tail[5]);
+    }
+    __syncthreads();
+    fixing = sh_flag != 0;
+    if (fixing) {
+      if (s == 0) {  // DynamoRIO: one class; this column group's k_total fix
+        if (live) {
+          fix_column(a.fx, M, col, a.segor);
+          fix_column(a.fx, M, col + 8, a.segor);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          st_sc1(&a.tail[kTailFixDone + bx], 1u);
+        }
+      } else if (threadIdx.x == 0) {
+        if (!spin_until(&a.tail[kTailFixDone + bx], 1u)) atomicOr(a.ca.err, 4u);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+    }
+  }
+  // ---- 2. the scan (k_scan's walk; prefixes from the segment ORs) --------------------------
+  {
+    uint4 prev = make_uint4(0, 0, 0, 0), send = prev, tot = prev;
+    // the segment ORs, 16 loads per round trip (unused segments are 0)
+    constexpr int SH = kMaxSeg / 2;
+    for (int h = 0; h < 2; h++) {
+      uint4 sv[SH];
+#pragma unroll
+      for (int q = 0; q < SH; q++)
+        sv[q] = *(const uint4 *)(a.segor + (size_t)(h * SH + q) * a.nclass * M + kc);
+#pragma unroll
+      for (int q = 0; q < SH; q++) {
+        const uint32_t ss = h * SH + q;
+        tot = or4(tot, sv[q]);
+        if (ss < s) prev = or4(prev, sv[q]);
+        if (ss <= s) send = or4(send, sv[q]);
+      }
+    }
+    const uint4 vir = *(const uint4 *)(a.vcur + kc);
+    const uint4 ig = *(const uint4 *)((a.ignore ? a.ignore : a.vcur) + col);
+    const uint32_t c0 = s * a.seg_len, c1 = min(a.nchunks, c0 + a.seg_len);
+    const uint32_t t0 = (bx * blockDim.x + (threadIdx.x & ~63u)) * 16 / kTileW;
+    const uint32_t cl0 = c0 + lane;
+    uint8_t ccls0 = 0;
+    uint64_t tfw0 = 0;
+    uint32_t lst0 = 0;
+    if (cl0 < c1) {
+      ccls0 = a.chunk_cls[cl0];
+      tfw0 = a.tflags[((size_t)cl0 * a.nclass + k) * a.nfw + (t0 >> 6)];
+      if (a.listed) lst0 = a.listed[cl0];
+    }
+    uint4 rel = make_uint4(~0u, ~0u, ~0u, ~0u);
+    if (a.ignore) {  // has_new_bits_with_ignore only examines bytes whose ignore byte is 0
+      const uint64_t m0 = nonzero_bytes8((uint64_t)ig.x | ((uint64_t)ig.y << 32));
+      const uint64_t m1 = nonzero_bytes8((uint64_t)ig.z | ((uint64_t)ig.w << 32));
+      rel = make_uint4(~(uint32_t)m0, ~(uint32_t)(m0 >> 32), ~(uint32_t)m1, ~(uint32_t)(m1 >> 32));
+    }
+    if (s == 0 && live) {
+      *(uint4 *)(a.vnext + kc) = make_uint4(vir.x & ~(tot.x & rel.x), vir.y & ~(tot.y & rel.y),
+                                            vir.z & ~(tot.z & rel.z), vir.w & ~(tot.w & rel.w));
+      if (k == a.nclass - 1)  // maps this mode does not use (DynamoRIO: tmout, crash) carry over
+        for (int kk = a.nclass; kk < 3; kk++)
+          *(uint4 *)(a.vnext + (size_t)kk * M + col) = *(const uint4 *)(a.vcur + (size_t)kk * M + col);
+    }
+    const uint4 vr = live ? make_uint4(vir.x & rel.x, vir.y & rel.y, vir.z & rel.z, vir.w & rel.w)
+                          : make_uint4(0, 0, 0, 0);
+    __shared__ uint64_t stage_buf[4][kWaveItems];
+    ItemStage stg{stage_buf[threadIdx.x >> 6], 0u};
+    __shared__ uint4 claim_q[4][kClaimQ];
+    ClaimQ cq{claim_q[threadIdx.x >> 6], 0};
+    const uint32_t seg_new = (send.x & vr.x & ~prev.x) | (send.y & vr.y & ~prev.y) |
+                             (send.z & vr.z & ~prev.z) | (send.w & vr.w & ~prev.w);
+    if (__ballot(seg_new != 0)) {  // wave-uniform
+      for (uint32_t cg = c0; cg < c1; cg += 64) {
+        const uint32_t cl = cg + lane;
+        bool any = false;
+        if (cg == c0) {
+          if (cl < c1 && ((ccls0 >> k) & 1)) any = lst0 || ((tfw0 >> (t0 & 63)) & 0xFull);
+        } else if (cl < c1 && ((a.chunk_cls[cl] >> k) & 1)) {
+          any = (a.listed && a.listed[cl]) ||
+                ((a.tflags[((size_t)cl * a.nclass + k) * a.nfw + (t0 >> 6)] >> (t0 & 63)) & 0xFull);
+        }
+        uint64_t mask = __ballot(any);
+        while (mask) {
+          uint32_t cs[KBZ_SCAN_ILP];
+#pragma unroll
+          for (int u = 0; u < KBZ_SCAN_ILP; u++) {
+            cs[u] = mask ? cg + (uint32_t)__builtin_ctzll(mask) : ~0u;
+            mask &= mask - 1;
+          }
+          uint4 o[KBZ_SCAN_ILP];
+          bool st[KBZ_SCAN_ILP];
+#pragma unroll
+          for (int u = 0; u < KBZ_SCAN_ILP; u++) {
+            const uint32_t c = cs[u] != ~0u ? cs[u] : cs[0];
+            o[u] = *(const uint4 *)(a.chunk_or + (size_t)c * a.nclass * M + kc);
+            st[u] = tile_stored(a.tflags, a.nfw, a.nclass, c, k, col) || (a.listed && a.listed[c]);
+          }
+#pragma unroll
+          for (int u = 0; u < KBZ_SCAN_ILP; u++) {
+            const uint32_t c = cs[u];  // uniform across the wave
+            if (c == ~0u) break;
+            if (!st[u]) o[u] = make_uint4(0, 0, 0, 0);
+            const uint4 nb = make_uint4(o[u].x & vr.x & ~prev.x, o[u].y & vr.y & ~prev.y,
+                                        o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
+            if (__ballot(nb.x | nb.y | nb.z | nb.w)) {
+              if (wave_claimed_bytes(nb) < a.win_items)
+                claims_enqueue(a.ca, k, cq, c, col, nb, vir, prev);
+              else
+                emit_items_wave(c, k, col, nb, vir, prev, stg, a.items, a.cap, a.counters,
+                                (uint8_t *)a.chunk_or + (size_t)c * a.nclass * M + kc, live,
+                                a.win_items);
+            }
+            prev = or4(prev, o[u]);
+          }
+        }
+      }
+      claims_flush(a.ca, k, cq);
+      flush_items(stg, a.items, a.cap, a.counters);
+    }
+  }
+  // ---- 3. help with the window items appended so far --------------------------------------
+  uint32_t *taken = &a.tail[1];
+  for (;;) {  // wave-uniform
+    uint32_t idx = ~0u;
+    if (lane == 0) {
+      for (;;) {
+        const uint32_t t = ld_sc1(taken), c = min(ld_sc1(&a.counters[0]), a.cap);
+        if (t >= c) break;
+        if (atomicCAS(taken, t, t + 1) == t) {
+          idx = t;
+          break;
+        }
+      }
+    }
+    idx = __shfl(idx, 0);
+    if (idx == ~0u) break;
+    uint64_t item = 0;
+    if (lane == 0)
+      for (uint32_t it = 0; it < kSpinMax && !(item = ld_sc1(&a.items[idx])); it++)
+        __builtin_amdgcn_s_sleep(1);
+    item = __shfl(item, 0);
+    if (!item) {
+      if (lane == 0) atomicOr(a.ca.err, 4u);
+      continue;
+    }
+    resolve_item(a.ra, item);
+    if (lane == 0) st_sc1(&a.items[idx], 0ull);
+  }
+  // ---- 4. the last workgroup: leftover items, scored rows -> hnb_out, re-arm ----------------
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics and sc1 stores are done
+  __syncthreads();
+  if (threadIdx.x == 0)
+    sh_flag = atomicAdd(&a.tail[0], 1u) == gridDim.x * gridDim.y * gridDim.z - 1;
+  __syncthreads();
+  if (!sh_flag) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const uint32_t nitems = min(ld_sc1(&a.counters[0]), a.cap);
+  for (uint32_t idx = ld_sc1(taken) + (threadIdx.x >> 6); idx < nitems; idx += blockDim.x / 64) {
+    const uint64_t item = ld_sc1(&a.items[idx]);  // every writer is done: no wait
+    if (!item) {
+      if (lane == 0) atomicOr(a.ca.err, 4u);
+      continue;
+    }
+    resolve_item(a.ra, item);
+    if (lane == 0) st_sc1(&a.items[idx], 0ull);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const uint32_t ntouched = ld_sc1(&a.tail[2]);
+  for (uint32_t i = threadIdx.x; i < ntouched; i += blockDim.x) {
+    const uint32_t row = ld_sc1(&a.ca.touched[i]);
+    const uint32_t h = ld_sc1(&a.ca.hnb32[row]);
+    if (a.hnb_out) a.hnb_out[row] = (uint8_t)h;
+    st_sc1(&a.ca.hnb32[row], 0u);
+  }
+  const uint32_t nfix = dr ? min(ld_sc1(a.fx.fix_cnt), a.nchunks) : 0u;
+  for (uint32_t i = threadIdx.x; i < nfix; i += blockDim.x) a.flags_w[a.fix_list_w[i]] = 0;
+  if (fixing)
+    for (uint32_t i = threadIdx.x; i < gridDim.x; i += blockDim.x) a.tail[kTailFixDone + i] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t *cn = a.counters;
+    a.err_out[0] = ld_sc1(&cn[1]);  // the sticky error flags, host-mapped (k_pack's role)
+    a.err_out[1] = ld_sc1(&cn[2]);
+    cn[8] = ld_sc1(&cn[0]);  // kbz_ctx_stats: claim items, recomputed chunks, bad rows
+    cn[9] = ld_sc1(&cn[3]);
+    cn[10] = ld_sc1(&cn[4]);
+    cn[0] = cn[3] = cn[4] = cn[5] = 0;
+    a.shard_last[0] = a.shard_last[1] = 0;
+    for (int i = 0; i < 6; i++) a.tail[i] = 0;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2720,7 +3128,11 @@ struct kbz_ctx {
   uint8_t *neq = nullptr;
   uint32_t *h32 = nullptr;
   uint32_t *hnb32 = nullptr;
-  uint8_t *segor = nullptr;
+  uint8_t *segor = nullptr;      // this batch's segment ORs (zero at batch start)
+  uint8_t *segor_alt = nullptr;  // the other buffer (the fused tail zeroes it and swaps)
+  uint32_t *tail = nullptr;      // k_tail's words (kTailFixDone + column groups)
+  uint32_t *touched = nullptr;   // [max_batch] rows the fused tail scored
+  bool fused_ok = true;          // one-shard batches through k_tail (KBZ_DEBUG_STAGED=1: staged)
   uint8_t *segprev = nullptr;
   uint8_t *total = nullptr;
   uint64_t *items = nullptr;
@@ -2828,7 +3240,8 @@ void free_ctx(kbz_ctx *c) {
   DevGuard g(c->device);
   void *ptrs[] = {c->V[0], c->V[1], c->last, c->ignore, c->chunk_or, c->chunk_cls, c->tflags,
                   c->flags, c->fix_list, c->bad_list, c->saved_row,
-                  c->skip, c->neq, c->h32, c->hnb32, c->segor, c->segprev, c->total,
+                  c->skip, c->neq, c->h32, c->hnb32, c->segor, c->segor_alt, c->tail,
+                  c->touched, c->segprev, c->total,
                   c->items, c->counters, c->shard_last, c->dslot[0], c->dslot[1],
                   c->dslot_oc[0], c->dslot_oc[1], c->dres_hnb, c->dres_h32, c->dres_x64};
   for (void *p : ptrs)
@@ -3033,6 +3446,8 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   if (const char *w = getenv("KBZ_DEBUG_WIN_ITEMS")) c->win_items = (uint32_t)std::max(1, atoi(w));
   // tests only: small AFL batches through the general pipeline instead of k_small
   if (const char *w = getenv("KBZ_DEBUG_NO_SMALL")) c->small_ok = atoi(w) == 0;
+  // tests only: one-shard batches through the staged kernels (k_chain ... k_pack) instead of k_tail
+  if (const char *w = getenv("KBZ_DEBUG_STAGED")) c->fused_ok = atoi(w) == 0;
   bool ok = !dalloc(&c->V[0], 3 * M) && !dalloc(&c->V[1], 3 * M) && !dalloc(&c->last, 2) &&
             !dalloc(&c->chunk_or, c->max_chunks * nc * M) && !dalloc(&c->chunk_cls, c->max_chunks) &&
             !dalloc(&c->tflags, c->max_chunks * nc * c->nfw) &&
@@ -3041,6 +3456,8 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
             !dalloc(&c->skip, max_batch) &&
             !dalloc(&c->neq, max_batch) && !dalloc(&c->h32, max_batch) &&
             !dalloc(&c->hnb32, max_batch) && !dalloc(&c->segor, kMaxSeg * nc * M) &&
+            !dalloc(&c->segor_alt, kMaxSeg * nc * M) &&
+            !dalloc(&c->tail, kTailFixDone + cdiv(M / 16, 256)) && !dalloc(&c->touched, max_batch) &&
             !dalloc(&c->segprev, kMaxSeg * nc * M) && !dalloc(&c->total, nc * M) &&
             !dalloc(&c->items, c->item_cap) && !dalloc(&c->counters, 16) &&
             !dalloc(&c->shard_last, 2);
@@ -3063,6 +3480,9 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   (void)hipMemset(c->shard_last, 0, 2 * sizeof(uint32_t));
   // consumers re-zero these for the next batch (k_total: segor, k_pack: hnb32)
   (void)hipMemset(c->segor, 0, kMaxSeg * nc * M);
+  (void)hipMemset(c->segor_alt, 0, kMaxSeg * nc * M);
+  (void)hipMemset(c->tail, 0, (kTailFixDone + cdiv(M / 16, 256)) * sizeof(uint32_t));
+  (void)hipMemset(c->items, 0, (size_t)c->item_cap * sizeof(uint64_t));  // zero between batches
   (void)hipMemset(c->hnb32, 0, max_batch * sizeof(uint32_t));
   (void)hipMemset(c->flags, 0, c->max_chunks * sizeof(uint32_t));
   if (hipDeviceSynchronize() != hipSuccess) {
@@ -3173,9 +3593,14 @@ int kbz_ctx_set_pass1(kbz_ctx_t *c, int choice) {
 }
 uint8_t *kbz_virgin_device(kbz_ctx_t *c) { return c ? c->V[c->vcur] : nullptr; }
 
-int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride,
-                    const int8_t *outcome, uint32_t *h32_out, uint64_t *x64_out, int want,
-                    void *stream) {
+}  // extern "C"
+namespace {
+int fused_link(kbz_ctx *c, hipStream_t s, SkipExtra *x);
+// kbz_shard_begin; with `fused` (a one-shard batch of kbz_triage_batch_device) pass 1 also
+// zeroes hnb_clear and k_skip takes k_chain's row-0 and saved-row roles (the fused tail).
+int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
+                     const int8_t *outcome, uint32_t *h32_out, uint64_t *x64_out, int want,
+                     void *stream, uint8_t *hnb_clear, bool fused) {
   if (!c) return fail("null ctx");
   if (n > c->max_batch) return fail("n exceeds max_batch");
   if (n && check_rows(traces, stride, c->M)) return -1;
@@ -3191,6 +3616,7 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
     HIP_TRY(hipMemsetAsync(c->shard_last, 0, 2 * sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(c->hnb32, 0, c->max_batch * sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(c->segor, 0, kMaxSeg * c->nc * c->M, s));
+    HIP_TRY(hipMemsetAsync(c->segor_alt, 0, kMaxSeg * c->nc * c->M, s));
     // kbz_shard_link may already have marked this batch's last row as the next row-0
     // predecessor, but V never received that batch: forget the row
     c->saved_valid = false;
@@ -3235,6 +3661,7 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
   a.vcur = c->V[c->vcur];
   a.tflags = c->tflags;
   a.nfw = c->nfw;
+  a.hnb_clear = hnb_clear;
   P1Ev pev;
   if (c->timing) {
     if (c->ev_used_n == c->ev_pass1.size()) {
@@ -3253,15 +3680,115 @@ int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride
     hipEvent_t st0;
     if (stage_begin(c, s, &st0)) return -1;
     const unsigned row_blocks = cdiv(n, 256);
-    hipLaunchKernelGGL(k_skip, dim3(row_blocks + c->cur_chunks - 1), dim3(256), 0, s, c->cur_h32,
-                       c->neq, (uint32_t)n, c->skip, c->flags, c->fix_list, c->counters + 3,
-                       c->bad_list, c->counters + 4, c->shard_last, traces, stride, c->ignore,
-                       (uint32_t)c->M, row_blocks);
+    SkipExtra x{};
+    unsigned extra = 0;
+    if (fused) {  // + row 0 and the saved-row copy (k_chain's jobs in the staged pipeline)
+      if (fused_link(c, s, &x)) return -1;
+      extra = 1 + x.copy_blocks;
+    }
+    hipLaunchKernelGGL(k_skip, dim3(row_blocks + c->cur_chunks - 1 + extra), dim3(256), 0, s,
+                       c->cur_h32, c->neq, (uint32_t)n, c->skip, c->flags, c->fix_list,
+                       c->counters + 3, c->bad_list, c->counters + 4, c->shard_last, traces,
+                       stride, c->ignore, (uint32_t)c->M, row_blocks, x);
     HIP_TRY(hipGetLastError());
     if (stage_end(c, s, KBZ_STAGE_SKIP, st0)) return -1;
   }
   c->stage = 1;
   return 0;
+}
+
+// The row-0 / saved-row arguments of a fused batch's k_skip and the context's chain bookkeeping
+// (kbz_shard_link for a one-shard batch): row 0's predecessor is the saved row (clean iff its
+// flag), the batch's last row becomes the next batch's predecessor (the other saved slot), the
+// next last hash goes to the other last-hash word; k_tail writes those two words.
+struct FusedChain {
+  uint32_t *ctx_last, *next_last, *saved_ok;
+};
+thread_local FusedChain g_fchain;
+int fused_link(kbz_ctx *c, hipStream_t, SkipExtra *x) {
+  const size_t M = c->M, n = c->cur_n;
+  x->row0_hp = c->last + c->lcur;
+  x->pred_saved = c->saved_valid ? 1 : 0;
+  x->pred_ok = c->counters + 6 + c->srow;
+  x->prow = c->saved_row + c->srow * M;
+  x->bad0 = c->tail + 4;
+  x->copy_src = c->cur_traces + (n - 1) * c->cur_stride;
+  x->copy_dst = c->saved_row + (c->srow ^ 1) * M;
+  x->copy_blocks = std::min(64u, cdiv(M / 16, 256));
+  g_fchain.ctx_last = c->last + c->lcur;
+  g_fchain.next_last = c->last + (c->lcur ^ 1);
+  g_fchain.saved_ok = c->counters + 6 + (c->srow ^ 1);
+  c->srow ^= 1;
+  c->saved_valid = true;
+  c->lcur ^= 1;
+  return 0;
+}
+
+// Everything after pass 1 (and k_skip) of a one-shard batch in one launch: k_tail.
+int fused_tail(kbz_ctx *c, uint8_t *hnb_out, hipStream_t s) {
+  const bool dr = c->mode == KBZ_MODE_DYNAMORIO;
+  const uint32_t n = (uint32_t)c->cur_n, M = (uint32_t)c->M;
+  const uint8_t *ign = dr ? c->ignore : nullptr;
+  const uint8_t *skip = dr ? c->skip : nullptr;
+  const int vn = c->vcur ^ 1;
+  TailArgs a{};
+  a.ca = ClaimArgs{c->cur_traces, c->cur_stride, n, c->mode, c->cur_outcome, skip, c->hnb32,
+                   c->counters + 2, c->touched, c->tail + 2};
+  a.ra = ResolveArgs{c->cur_traces, c->cur_stride, n, c->mode, c->cur_outcome, skip, c->hnb32,
+                     c->counters + 2, c->chunk_or, c->nc, M, c->V[c->vcur], ign, c->touched,
+                     c->tail + 2};
+  a.fx = FixArgs{c->cur_traces, c->cur_stride, n, c->skip, c->fix_list, c->counters + 3,
+                 c->chunk_or, c->chunk_cls, c->cur_chunks, c->cur_seg_len, c->flags, c->tflags,
+                 c->nfw};
+  a.chunk_or = c->chunk_or;
+  a.chunk_cls = c->chunk_cls;
+  a.nchunks = c->cur_chunks;
+  a.seg_len = c->cur_seg_len;
+  a.nseg = c->cur_nseg;
+  a.nclass = c->nc;
+  a.map_size = M;
+  a.segor = c->segor;
+  a.segor_next = c->segor_alt;
+  a.vcur = c->V[c->vcur];
+  a.vnext = c->V[vn];
+  a.ignore = ign;
+  a.items = c->items;
+  a.cap = c->item_cap;
+  a.counters = c->counters;
+  a.tflags = c->tflags;
+  a.nfw = c->nfw;
+  a.listed = dr ? c->flags : nullptr;
+  a.win_items = c->win_items;
+  a.hnb_out = hnb_out;
+  a.tail = c->tail;
+  a.err_out = c->d_err;
+  a.shard_last = c->shard_last;
+  a.neq = c->neq;
+  a.bad_list = c->bad_list;
+  a.ctx_last = g_fchain.ctx_last;
+  a.next_last = g_fchain.next_last;
+  a.saved_ok = g_fchain.saved_ok;
+  a.flags_w = c->flags;
+  a.fix_list_w = c->fix_list;
+  a.fix_cnt_w = c->counters + 3;
+  hipEvent_t st0;
+  if (stage_begin(c, s, &st0)) return -1;
+  hipLaunchKernelGGL(k_tail, dim3(cdiv(M / 16, 256), c->cur_nseg, c->nc), dim3(256), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  if (stage_end(c, s, KBZ_STAGE_SCAN, st0)) return -1;
+  std::swap(c->segor, c->segor_alt);
+  c->vcur = vn;
+  c->stage = 0;
+  return 0;
+}
+}  // namespace
+extern "C" {
+
+int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride,
+                    const int8_t *outcome, uint32_t *h32_out, uint64_t *x64_out, int want,
+                    void *stream) {
+  return shard_begin_impl(c, traces, n, stride, outcome, h32_out, x64_out, want, stream, nullptr,
+                          false);
 }
 
 int kbz_shard_last_hash(kbz_ctx_t *c, uint32_t *d_out, void *stream) {
@@ -3412,16 +3939,17 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
                      c->mode == KBZ_MODE_DYNAMORIO ? c->flags : nullptr, c->win_items,
                      ClaimArgs{c->cur_traces, c->cur_stride, (uint32_t)c->cur_n, c->mode,
                                c->cur_outcome, c->mode == KBZ_MODE_DYNAMORIO ? c->skip : nullptr,
-                               c->hnb32, c->counters + 2});
+                               c->hnb32, c->counters + 2, nullptr, nullptr});
   HIP_TRY(hipGetLastError());
   if (stage_end(c, s, KBZ_STAGE_SCAN, st0)) return -1;
   if (c->cur_n) {
     if (stage_begin(c, s, &st0)) return -1;
-    hipLaunchKernelGGL(k_resolve, dim3(512), dim3(256), 0, s, c->cur_traces, c->cur_stride,
-                       (uint32_t)c->cur_n, c->mode, c->cur_outcome,
-                       c->mode == KBZ_MODE_DYNAMORIO ? c->skip : nullptr, c->items, c->counters,
-                       c->item_cap, c->hnb32, c->counters + 2, c->chunk_or, c->nc,
-                       (uint32_t)c->M, c->V[c->vcur], ign);
+    hipLaunchKernelGGL(k_resolve, dim3(512), dim3(256), 0, s,
+                       ResolveArgs{c->cur_traces, c->cur_stride, (uint32_t)c->cur_n, c->mode,
+                                   c->cur_outcome, c->mode == KBZ_MODE_DYNAMORIO ? c->skip : nullptr,
+                                   c->hnb32, c->counters + 2, c->chunk_or, c->nc, (uint32_t)c->M,
+                                   c->V[c->vcur], ign, nullptr, nullptr},
+                       c->items, c->counters, c->item_cap);
     HIP_TRY(hipGetLastError());
     if (stage_end(c, s, KBZ_STAGE_RESOLVE, st0)) return -1;
     if (stage_begin(c, s, &st0)) return -1;
@@ -3462,6 +3990,13 @@ int kbz_triage_batch_device(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_
     HIP_TRY(hipGetLastError());
     c->vcur = vn;
     return 0;
+  }
+  if (c && c->fused_ok && n && c->stage == 0) {  // one shard: pass 1, [k_skip], k_tail
+    if (shard_begin_impl(c, traces, n, stride, outcome, h32_out, x64_out, want, stream, hnb_out,
+                         true))
+      return -1;
+    DevGuard g(c->device);
+    return fused_tail(c, hnb_out, (hipStream_t)stream);
   }
   if (kbz_shard_begin(c, traces, n, stride, outcome, h32_out, x64_out, want, stream)) return -1;
   if (kbz_shard_link(c, nullptr, nullptr, 1, nullptr, nullptr, stream)) return -1;

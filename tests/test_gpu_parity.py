@@ -18,13 +18,19 @@ pytestmark = pytest.mark.gpu
 MODES = [MODE_AFL, MODE_DYNAMORIO, MODE_AFL_CLASSIFY]
 
 
-@pytest.fixture(autouse=True, params=["narrow", "wide"])
+@pytest.fixture(autouse=True, params=["narrow", "wide", "narrow-staged"])
 def pass1(request, monkeypatch):
     """Every case runs through both pass-1 kernels: k_pass1s (narrow; what AUTO picks for
-    batches of >= 512 chunks, e.g. config 2) and k_pass1w (wide; AUTO's pick below that).
-    kbz_ctx_create reads KBZ_PASS1 as the new context's default."""
-    monkeypatch.setenv("KBZ_PASS1", request.param)
-    return request.param
+    batches of >= 512 chunks, e.g. config 2) and k_pass1w (wide; AUTO's pick below that), and
+    through both tails after pass 1: the fused one-shard tail (k_skip + k_tail, what
+    kbz_triage_batch_device runs) and the staged kernels the sharded protocol runs (k_skip,
+    k_chain, k_total, k_scan, k_resolve, k_pack; KBZ_DEBUG_STAGED=1).  kbz_ctx_create reads
+    KBZ_PASS1 / KBZ_DEBUG_STAGED as the new context's defaults."""
+    kind = request.param.split("-")[0]
+    monkeypatch.setenv("KBZ_PASS1", kind)
+    if request.param.endswith("staged"):
+        monkeypatch.setenv("KBZ_DEBUG_STAGED", "1")
+    return kind
 
 
 def gpu_triage(ctx, traces, oc, want=WANT_H32 | WANT_X64):

@@ -387,10 +387,10 @@ def test_dynamorio_resume(gpu, per_module):
     # set_state after the first exec: the loaded maps are kept (fuzzer_id is set by then)
     b.set_state(st)
     r = b.triage_batch(rows[n:], hashes=False)
-    np.testing.assert_array_equal(r["hnb"], np.any([e["hnb"] != 0 for e in old], axis=0))
+    np.testing.assert_array_equal(r["hnb"] != 0, np.any([e["hnb"] != 0 for e in old], axis=0))
     # the batched member resets too, on its first exec
     c = P.Plugin("dynamorio_gpu", opts, st)
-    np.testing.assert_array_equal(c.triage_batch(rows[n:], hashes=False)["hnb"], want)
+    np.testing.assert_array_equal(c.triage_batch(rows[n:], hashes=False)["hnb"] != 0, want)
     # no exec, no enable: a loaded state merges with its maps
     d = P.Plugin("dynamorio_gpu", opts, st)
     m = d.merge(P.Plugin("dynamorio_gpu", opts))
