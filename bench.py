@@ -537,11 +537,8 @@ def main_triage(args):
     phase_log = None  # list: per-batch phase timings of the sharded protocol (world > 1)
 
     def step(t, oc):
-        if world == 1:
-            ctx.shard_begin(t, oc, want, out=out)
-            ctx.shard_link(None, None, True, None, None)
-            ctx.shard_reduce()
-            ctx.shard_finish(None, None)  # single shard: its own aggregate is the total
+        if world == 1:  # one shard: kbz_triage_batch_device (pass 1, k_skip, k_tail, k_fin)
+            ctx.triage(t, oc, want, out=out)
         else:
             triage_sharded(ctx, t, oc, counts, rank, world, want, device=dev, timings=phase_log)
 

@@ -118,7 +118,10 @@ int kbz_ctx_time_pass1(kbz_ctx_t *ctx, int enable, double *total_ms, uint32_t *l
 /* The same for the pipeline's other stages (k_skip, k_chain, k_total, k_scan, k_resolve,
  * k_pack): stage_ms[KBZ_NSTAGES] gets each stage's summed duration over the batches timed since
  * the previous call (index KBZ_STAGE_*; pass 1 stays with kbz_ctx_time_pass1, slot 0 is 0),
- * *batches how many batches finished.  Diagnostics only (bench.py). */
+ * *batches how many batches finished (one KBZ_STAGE_SCAN record each; the fused one-shard tail,
+ * k_tail, is recorded as KBZ_STAGE_SCAN).  Past 512 pending records the oldest are folded into
+ * running sums (both calls), so timing left on without reads keeps a bounded event pool.
+ * Diagnostics only (bench.py). */
 enum kbz_stage { KBZ_STAGE_PASS1 = 0, KBZ_STAGE_SKIP = 1, KBZ_STAGE_LINK = 2, KBZ_STAGE_REDUCE = 3,
                  KBZ_STAGE_SCAN = 4, KBZ_STAGE_RESOLVE = 5, KBZ_STAGE_PACK = 6, KBZ_NSTAGES = 7 };
 int kbz_ctx_time_stages(kbz_ctx_t *ctx, int enable, double *stage_ms, uint32_t *batches);

@@ -1473,16 +1473,19 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
     // ------------------------------------------------------------ N: the neighbour test
     uint64_t nacc = 0;  // OR over the row's words of (word ^ previous row's word)
     const uint4 *ring = IGN ? wring : kring;
+    KBZ_STAMP_DECL;  // N: {compare, ready wait, LDS read wait, -}
     for (uint32_t t0 = 0; t0 < ntiles; t0 += RING)
       static_for<RING>([&](auto sc) {  // slots as compile-time constants (see C)
       constexpr int sl = decltype(sc)::value;
       const uint32_t t = t0 + sl;
       if (t >= ntiles) return;
       wait_ready(t);
+      KBZ_STAMP(1);
       uint4 vv[SLOTS];
 #pragma unroll
       for (int q = 0; q < SLOTS; q++) vv[q] = ring[sl * TILE + lane * SLOTS + (q ^ sw)];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      KBZ_STAMP(2);
       if (lane == 0) KBZ_FST(freed_n, sl, (int)t);
 #pragma unroll
       for (int q = 0; q < SLOTS; q++) {
@@ -1490,7 +1493,9 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
         const uint64_t w1 = (uint64_t)vv[q].z | ((uint64_t)vv[q].w << 32);
         nacc |= (w0 ^ from_prev_lane(w0)) | (w1 ^ from_prev_lane(w1));
       }
+      KBZ_STAMP(0);
     });
+    KBZ_STAMP_FLUSH(chunk * 16 + wave);
     // lane 0 has no predecessor in the wave: a placeholder (k_skip compares chunk starts)
     if (lane < nrows) a.neq[row0 + lane] = nacc != 0;
   } else if ((wave & 3) == 0) {
@@ -1935,16 +1940,10 @@ __device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
 __device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// A claim's score for trace `row` (has_new_bits' 1 or 2, the maximum over its claims).  With a
-// touched list (the fused tail) the first scorer of a row also lists it, so the tail's last
-// workgroup copies only scored rows into hnb_out (pass 1 zeroed the others).
-__device__ __forceinline__ void score_row(uint32_t *hnb32, uint32_t *touched, uint32_t *tcount,
-                                          uint64_t row, uint32_t v) {
-  if (!touched) {
-    atomicMax(&hnb32[row], v);
-    return;
-  }
-  if (atomicMax(&hnb32[row], v) == 0u) st_sc1(&touched[atomicAdd(tcount, 1u)], (uint32_t)row);
+// A claim's score for trace `row` (has_new_bits' 1 or 2, the maximum over its claims):
+// fire-and-forget, the outputs are copied once every score is final (k_pack / k_fin).
+__device__ __forceinline__ void score_row(uint32_t *hnb32, uint64_t row, uint32_t v) {
+  atomicMax(&hnb32[row], v);
 }
 
 // Append this lane's claim items (one per nonzero byte of nb) with ONE atomic per wave:
@@ -2050,8 +2049,6 @@ struct ClaimArgs {  // what k_scan needs to resolve claims inline (k_resolve's i
   const uint8_t *skip;
   uint32_t *hnb32;
   uint32_t *err;
-  uint32_t *touched;  // fused tail: rows scored so far (null: the staged pipeline's k_pack)
-  uint32_t *tcount;
 };
 __device__ __forceinline__ uint32_t pick4(uint4 v, int i) {  // i wave-uniform
   return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
@@ -2103,7 +2100,7 @@ __device__ __forceinline__ void claims_flush(const ClaimArgs &ca, int k, ClaimQ 
     }
     if ((claimers >> lane) & 1) {
       const bool two = (e[j].z >> 8) && first_nz && (lane == __builtin_ctzll(first_nz));
-      score_row(ca.hnb32, ca.touched, ca.tcount, row, two ? 2u : 1u);
+      score_row(ca.hnb32, row, two ? 2u : 1u);
     }
   }
   asm volatile("" ::: "memory");
@@ -2303,8 +2300,6 @@ struct ResolveArgs {  // what resolving a claim item needs (k_resolve, the fused
   uint32_t map_size;
   const uint8_t *vcur;
   const uint8_t *ignore;
-  uint32_t *touched;  // see ClaimArgs
-  uint32_t *tcount;
 };
 __device__ __forceinline__ void resolve_window(const ResolveArgs &r, uint32_t chunk, int k,
                                                uint32_t wcol, const uint8_t *win_prev) {
@@ -2358,11 +2353,11 @@ __device__ __forceinline__ void resolve_window(const ResolveArgs &r, uint32_t ch
       const uint32_t sc = __ballot(two) ? 2u : __ballot(nw) ? 1u : 0u;
       if (sc) {
         claimed = true;
-        if (lane == 0) score_row(r.hnb32, r.touched, r.tcount, row0 + rr[u], sc);
+        if (lane == 0) score_row(r.hnb32, row0 + rr[u], sc);
       }
     }
   }
-  if (!claimed && lane == 0) atomicOr(r.err, 2u);  // k_scan saw new bits here: inconsistent
+  if (!claimed && lane == 0) atomicOr(r.err, 8u);  // k_scan saw new bits here: inconsistent
 }
 
 // One claim item (wave-uniform): a window item (new bits field 0) or one claimed byte of one
@@ -2393,14 +2388,14 @@ __device__ __forceinline__ void resolve_item(const ResolveArgs &r, uint64_t item
     if ((nb >> b) & 1) {
       const uint64_t m = __ballot((tb >> b) & 1);
       if (!m) {
-        if (lane == 0) atomicOr(r.err, 2u);
+        if (lane == 0) atomicOr(r.err, 16u);
       }
       claimers |= m & (0 - m);
     }
   }
   if ((claimers >> lane) & 1) {
     const bool two = f2 && first_nz && (lane == __builtin_ctzll(first_nz));
-    score_row(r.hnb32, r.touched, r.tcount, row, two ? 2u : 1u);
+    score_row(r.hnb32, row, two ? 2u : 1u);
   }
 }
 
@@ -2455,17 +2450,17 @@ __global__ void k_pack(uint32_t *hnb32, const uint32_t *h32, uint32_t n, uint8_t
 //      workgroup of lower linear index, which was dispatched first: no deadlock at any grid size);
 //   2. k_scan's walk, with the segment prefixes taken from the segment ORs themselves (all 32
 //      loads in one round trip) instead of k_total's output; segment 0 writes V' = V & ~total;
-//   3. resolves the window items appended so far (claims it with a CAS on the taken counter);
-//   4. takes a ticket; the LAST workgroup resolves the items nobody took, copies the scored rows
-//      (a touched list: the first scorer of each row appends it) into hnb_out -- pass 1 zeroed
-//      the others -- and re-arms the per-batch state.
+//   3. appends the claims it does not resolve inline as items for k_fin (the next launch), which
+//      resolves them over a wide grid and copies the scores into hnb_out once they are final,
+//      then re-arms the per-batch state.
 // It also zeroes the other segment-OR buffer for the next batch (segor is double-buffered).
 // Hand-offs between workgroups use agent-scope atomics or sc1 stores/loads (score_row, st_sc1,
 // ld_sc1); the rare fix path publishes plain stores with release / acquire fences.
 // ---------------------------------------------------------------------------------------------
-constexpr int kTailFixDone = 16;  // tail words: [0] ticket [1] taken [2] touched [3] walks done
+constexpr int kTailFixDone = 16;  // tail words: [0] ticket (k_fin) [3] walks done
                                   // [4] bad0 (k_skip) [5] fixing [16 + bx] column group bx fixed
 constexpr uint32_t kSpinMax = 1u << 22;
+
 __device__ __forceinline__ bool spin_until(const uint32_t *p, uint32_t want) {
   for (uint32_t it = 0; it < kSpinMax; it++) {
     if (ld_sc1(p) == want) return true;
@@ -2474,7 +2469,7 @@ __device__ __forceinline__ bool spin_until(const uint32_t *p, uint32_t want) {
   return false;
 }
 struct TailArgs {
-  ClaimArgs ca;         // traces, stride, n, mode, outcome, skip, hnb32, err, touched, tcount
+  ClaimArgs ca;         // traces, stride, n, mode, outcome, skip, hnb32, err
   ResolveArgs ra;
   FixArgs fx;           // DynamoRIO fix path (fx.fix_cnt = counters + 3)
   uint8_t *chunk_or;
@@ -2494,9 +2489,7 @@ struct TailArgs {
   uint32_t nfw;
   const uint32_t *listed;  // DynamoRIO: fix-list flags
   uint32_t win_items;
-  uint8_t *hnb_out;
   uint32_t *tail;
-  uint32_t *err_out;       // host-mapped copy of counters[1..2]
   uint32_t *shard_last;
   // DynamoRIO chain bookkeeping of k_chain (one shard)
   const uint8_t *neq;
@@ -2545,7 +2538,7 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
       }
     }
     if (threadIdx.x == 0) {
-      if (!spin_until(&a.tail[3], 1u)) atomicOr(a.ca.err, 4u);
+      if (!spin_until(&a.tail[3], 1u)) atomicOr(a.ca.err, 32u);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       sh_flag = (int)ld_sc1(&a.tail[5]);
@@ -2566,7 +2559,7 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
           st_sc1(&a.tail[kTailFixDone + bx], 1u);
         }
       } else if (threadIdx.x == 0) {
-        if (!spin_until(&a.tail[kTailFixDone + bx], 1u)) atomicOr(a.ca.err, 4u);
+        if (!spin_until(&a.tail[kTailFixDone + bx], 1u)) atomicOr(a.ca.err, 32u);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -2674,69 +2667,93 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
       flush_items(stg, a.items, a.cap, a.counters);
     }
   }
-  // ---- 3. help with the window items appended so far --------------------------------------
-  uint32_t *taken = &a.tail[1];
-  for (;;) {  // wave-uniform
-    uint32_t idx = ~0u;
-    if (lane == 0) {
-      for (;;) {
-        const uint32_t t = ld_sc1(taken), c = min(ld_sc1(&a.counters[0]), a.cap);
-        if (t >= c) break;
-        if (atomicCAS(taken, t, t + 1) == t) {
-          idx = t;
-          break;
-        }
+  // Window and byte items are resolved by k_fin, the next launch: helping with them here, while
+  // other workgroups still scan, read stale column windows on gfx950 (the running OR a window
+  // item leaves over its chunk's column window, stored sc1 and drained before the item was
+  // published, read back sc1 after an agent-scope acquire) -- 8 of 11 fused parity cases raised
+  // inconsistent-claim flags; after a launch boundary they are exact.
+}
+
+// The second launch of the fused tail.  Scores are fire-and-forget atomicMax into hnb32 (k_tail's
+// inline claims, then these items); the outputs are copied once every score is final:
+//   - no claim items (the common case: fresh batches on a warm map, every claim inline): k_tail
+//     was the previous launch, so every workgroup copies its slice of the rows at once;
+//   - otherwise the items are resolved over the whole grid (k_resolve's work) and the LAST
+//     workgroup (an agent-scope ticket after each workgroup's drained atomics) copies all rows
+//     with sc1 loads (k_pack's role).
+// The last workgroup also clears the fix-list flags and re-arms the per-batch words.
+struct FinArgs {
+  ResolveArgs ra;
+  uint64_t *items;
+  uint32_t cap;
+  uint32_t *counters;
+  uint32_t *tail;
+  uint32_t tail_fix_words;  // k_tail's column groups (its fix-done flags)
+  uint8_t *hnb_out;
+  uint32_t *err_out;
+  uint32_t *shard_last;
+  uint32_t *flags_w;
+  const uint32_t *fix_list_w;
+  const uint32_t *fix_cnt;  // null: AFL modes (no fix list)
+  uint32_t nchunks;
+};
+__device__ __forceinline__ void fin_copy_rows(const FinArgs &a, uint32_t j0, uint32_t step, bool sc1) {
+  // 4 rows per thread per step (one 16-B load of hnb32), j0 a multiple of 4
+  const uint32_t n = a.ra.n;
+  for (uint32_t j = j0; j < n; j += step) {
+    uint32_t h[4];
+    if (j + 4 <= n && !sc1) {
+      const uint4 v = *(const uint4 *)(a.ra.hnb32 + j);
+      h[0] = v.x, h[1] = v.y, h[2] = v.z, h[3] = v.w;
+      *(uint4 *)(a.ra.hnb32 + j) = make_uint4(0, 0, 0, 0);
+    } else {
+      for (int u = 0; u < 4; u++) {
+        h[u] = j + u < n ? (sc1 ? ld_sc1(&a.ra.hnb32[j + u]) : a.ra.hnb32[j + u]) : 0u;
+        if (j + u < n) a.ra.hnb32[j + u] = 0;
       }
     }
-    idx = __shfl(idx, 0);
-    if (idx == ~0u) break;
-    uint64_t item = 0;
-    if (lane == 0)
-      for (uint32_t it = 0; it < kSpinMax && !(item = ld_sc1(&a.items[idx])); it++)
-        __builtin_amdgcn_s_sleep(1);
-    item = __shfl(item, 0);
-    if (!item) {
-      if (lane == 0) atomicOr(a.ca.err, 4u);
-      continue;
+    if (a.hnb_out) {
+      if (j + 4 <= n && !((uintptr_t)(a.hnb_out + j) & 3))
+        *(uint32_t *)(a.hnb_out + j) = h[0] | (h[1] << 8) | (h[2] << 16) | (h[3] << 24);
+      else
+        for (int u = 0; u < 4; u++)
+          if (j + u < n) a.hnb_out[j + u] = (uint8_t)h[u];
     }
-    resolve_item(a.ra, item);
-    if (lane == 0) st_sc1(&a.items[idx], 0ull);
   }
-  // ---- 4. the last workgroup: leftover items, scored rows -> hnb_out, re-arm ----------------
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics and sc1 stores are done
+}
+__global__ __launch_bounds__(256) void k_fin(FinArgs a) {
+  __shared__ int last;
+  const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t wave = gtid >> 6;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t cnt = min(a.counters[0], a.cap);  // k_tail's appends: an earlier launch
+  if (cnt == 0) {
+    fin_copy_rows(a, 4 * gtid, 4 * gridDim.x * blockDim.x, false);
+  } else {
+    for (uint32_t it = wave; it < cnt; it += nwaves) {
+      const uint64_t item = a.items[it];
+      if (!item) {  // reserved and never written
+        if ((threadIdx.x & 63) == 0) atomicOr(a.ra.err, 64u);
+        continue;
+      }
+      resolve_item(a.ra, item);
+      if ((threadIdx.x & 63) == 0) a.items[it] = 0;  // the list is all-zero between batches
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics and stores are done
   __syncthreads();
-  if (threadIdx.x == 0)
-    sh_flag = atomicAdd(&a.tail[0], 1u) == gridDim.x * gridDim.y * gridDim.z - 1;
+  if (threadIdx.x == 0) last = atomicAdd(&a.tail[0], 1u) == gridDim.x - 1;
   __syncthreads();
-  if (!sh_flag) return;
+  if (!last) return;
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  const uint32_t nitems = min(ld_sc1(&a.counters[0]), a.cap);
-  for (uint32_t idx = ld_sc1(taken) + (threadIdx.x >> 6); idx < nitems; idx += blockDim.x / 64) {
-    const uint64_t item = ld_sc1(&a.items[idx]);  // every writer is done: no wait
-    if (!item) {
-      if (lane == 0) atomicOr(a.ca.err, 4u);
-      continue;
-    }
-    resolve_item(a.ra, item);
-    if (lane == 0) st_sc1(&a.items[idx], 0ull);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const uint32_t ntouched = ld_sc1(&a.tail[2]);
-  for (uint32_t i = threadIdx.x; i < ntouched; i += blockDim.x) {
-    const uint32_t row = ld_sc1(&a.ca.touched[i]);
-    const uint32_t h = ld_sc1(&a.ca.hnb32[row]);
-    if (a.hnb_out) a.hnb_out[row] = (uint8_t)h;
-    st_sc1(&a.ca.hnb32[row], 0u);
-  }
-  const uint32_t nfix = dr ? min(ld_sc1(a.fx.fix_cnt), a.nchunks) : 0u;
+  if (cnt) fin_copy_rows(a, 4 * threadIdx.x, 4 * blockDim.x, true);
+  const uint32_t nfix = a.fix_cnt ? min(ld_sc1(a.fix_cnt), a.nchunks) : 0u;
   for (uint32_t i = threadIdx.x; i < nfix; i += blockDim.x) a.flags_w[a.fix_list_w[i]] = 0;
-  if (fixing)
-    for (uint32_t i = threadIdx.x; i < gridDim.x; i += blockDim.x) a.tail[kTailFixDone + i] = 0;
+  for (uint32_t i = threadIdx.x; i < a.tail_fix_words; i += blockDim.x) a.tail[kTailFixDone + i] = 0;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t *cn = a.counters;
@@ -3131,7 +3148,6 @@ struct kbz_ctx {
   uint8_t *segor = nullptr;      // this batch's segment ORs (zero at batch start)
   uint8_t *segor_alt = nullptr;  // the other buffer (the fused tail zeroes it and swaps)
   uint32_t *tail = nullptr;      // k_tail's words (kTailFixDone + column groups)
-  uint32_t *touched = nullptr;   // [max_batch] rows the fused tail scored
   bool fused_ok = true;          // one-shard batches through k_tail (KBZ_DEBUG_STAGED=1: staged)
   uint8_t *segprev = nullptr;
   uint8_t *total = nullptr;
@@ -3188,6 +3204,8 @@ struct kbz_ctx {
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pass1;
   size_t ev_used_n = 0;
+  double pass1_folded_ms = 0;  // launches folded out of the event pool (kEvFoldAt)
+  uint32_t pass1_folded_n = 0;
   // kbz_ctx_time_stages: HIP events around the other stages' launches (stage id, start, end)
   bool stage_timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -3197,6 +3215,8 @@ struct kbz_ctx {
     hipEvent_t a, b;
   };
   std::vector<StageRec> stage_recs;
+  double stage_folded_ms[KBZ_NSTAGES] = {};
+  uint32_t stage_folded_nb = 0;
 };
 
 namespace {
@@ -3241,7 +3261,7 @@ void free_ctx(kbz_ctx *c) {
   void *ptrs[] = {c->V[0], c->V[1], c->last, c->ignore, c->chunk_or, c->chunk_cls, c->tflags,
                   c->flags, c->fix_list, c->bad_list, c->saved_row,
                   c->skip, c->neq, c->h32, c->hnb32, c->segor, c->segor_alt, c->tail,
-                  c->touched, c->segprev, c->total,
+                  c->segprev, c->total,
                   c->items, c->counters, c->shard_last, c->dslot[0], c->dslot[1],
                   c->dslot_oc[0], c->dslot_oc[1], c->dres_hnb, c->dres_h32, c->dres_x64};
   for (void *p : ptrs)
@@ -3372,10 +3392,38 @@ int pass1_dispatch(kbz_ctx *c, const Pass1Args &a, uint32_t chunks, bool x64, bo
   return 0;
 }
 
+// A caller that enables timing and never reads it must not grow the event pools without bound:
+// past kEvFoldAt records the oldest ones are read (their end events waited for) and folded into
+// running sums that the next kbz_ctx_time_* call reports with the rest.
+constexpr size_t kEvFoldAt = 512;
+int fold_pass1(kbz_ctx *c) {
+  for (size_t i = 0; i < c->ev_used_n; i++) {
+    HIP_TRY(hipEventSynchronize(c->ev_pass1[i].second));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev_pass1[i].first, c->ev_pass1[i].second));
+    c->pass1_folded_ms += ms;
+  }
+  c->pass1_folded_n += (uint32_t)c->ev_used_n;
+  c->ev_used_n = 0;
+  return 0;
+}
+int fold_stages(kbz_ctx *c) {
+  for (const auto &r : c->stage_recs) {
+    HIP_TRY(hipEventSynchronize(r.b));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
+    c->stage_folded_ms[r.stage] += ms;
+    c->stage_folded_nb += r.stage == KBZ_STAGE_SCAN;
+  }
+  c->stage_recs.clear();
+  c->ev_pool_used = 0;
+  return 0;
+}
 // Stage timing (kbz_ctx_time_stages): a start event now, the end event at stage_end.
 int stage_begin(kbz_ctx *c, hipStream_t s, hipEvent_t *out) {
   *out = nullptr;
   if (!c->stage_timing) return 0;
+  if (c->ev_pool_used + 2 > 2 * kEvFoldAt && fold_stages(c)) return -1;
   if (c->ev_pool_used + 2 > c->ev_pool.size()) {
     for (int i = 0; i < 2; i++) {
       hipEvent_t e;
@@ -3457,7 +3505,7 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
             !dalloc(&c->neq, max_batch) && !dalloc(&c->h32, max_batch) &&
             !dalloc(&c->hnb32, max_batch) && !dalloc(&c->segor, kMaxSeg * nc * M) &&
             !dalloc(&c->segor_alt, kMaxSeg * nc * M) &&
-            !dalloc(&c->tail, kTailFixDone + cdiv(M / 16, 256)) && !dalloc(&c->touched, max_batch) &&
+            !dalloc(&c->tail, kTailFixDone + cdiv(M / 16, 256)) &&
             !dalloc(&c->segprev, kMaxSeg * nc * M) && !dalloc(&c->total, nc * M) &&
             !dalloc(&c->items, c->item_cap) && !dalloc(&c->counters, 16) &&
             !dalloc(&c->shard_last, 2);
@@ -3552,36 +3600,23 @@ int kbz_ctx_stats(kbz_ctx_t *c, uint32_t *out) {
 int kbz_ctx_time_pass1(kbz_ctx_t *c, int enable, double *total_ms, uint32_t *launches) {
   if (!c) return fail("null ctx");
   DevGuard g(c->device);
-  double sum = 0;
-  for (size_t i = 0; i < c->ev_used_n; i++) {
-    HIP_TRY(hipEventSynchronize(c->ev_pass1[i].second));
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, c->ev_pass1[i].first, c->ev_pass1[i].second));
-    sum += ms;
-  }
-  if (total_ms) *total_ms = sum;
-  if (launches) *launches = (uint32_t)c->ev_used_n;
-  c->ev_used_n = 0;
+  if (fold_pass1(c)) return -1;
+  if (total_ms) *total_ms = c->pass1_folded_ms;
+  if (launches) *launches = c->pass1_folded_n;
+  c->pass1_folded_ms = 0;
+  c->pass1_folded_n = 0;
   c->timing = enable != 0;
   return 0;
 }
 int kbz_ctx_time_stages(kbz_ctx_t *c, int enable, double *stage_ms, uint32_t *batches) {
   if (!c) return fail("null ctx");
   DevGuard g(c->device);
-  double sum[KBZ_NSTAGES] = {0};
-  uint32_t nb = 0;
-  for (const auto &r : c->stage_recs) {
-    HIP_TRY(hipEventSynchronize(r.b));
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
-    sum[r.stage] += ms;
-    nb += r.stage == KBZ_STAGE_PACK;
-  }
+  if (fold_stages(c)) return -1;
   if (stage_ms)
-    for (int i = 0; i < KBZ_NSTAGES; i++) stage_ms[i] = sum[i];
-  if (batches) *batches = nb;
-  c->stage_recs.clear();
-  c->ev_pool_used = 0;
+    for (int i = 0; i < KBZ_NSTAGES; i++) stage_ms[i] = c->stage_folded_ms[i];
+  if (batches) *batches = c->stage_folded_nb;
+  for (int i = 0; i < KBZ_NSTAGES; i++) c->stage_folded_ms[i] = 0;
+  c->stage_folded_nb = 0;
   c->stage_timing = enable != 0;
   return 0;
 }
@@ -3664,6 +3699,7 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
   a.hnb_clear = hnb_clear;
   P1Ev pev;
   if (c->timing) {
+    if (c->ev_used_n >= kEvFoldAt && fold_pass1(c)) return -1;
     if (c->ev_used_n == c->ev_pass1.size()) {
       std::pair<hipEvent_t, hipEvent_t> e;
       // device-scope release: the default system-scope fence adds ~13 us per batch on MI355X
@@ -3733,10 +3769,9 @@ int fused_tail(kbz_ctx *c, uint8_t *hnb_out, hipStream_t s) {
   const int vn = c->vcur ^ 1;
   TailArgs a{};
   a.ca = ClaimArgs{c->cur_traces, c->cur_stride, n, c->mode, c->cur_outcome, skip, c->hnb32,
-                   c->counters + 2, c->touched, c->tail + 2};
+                   c->counters + 2};
   a.ra = ResolveArgs{c->cur_traces, c->cur_stride, n, c->mode, c->cur_outcome, skip, c->hnb32,
-                     c->counters + 2, c->chunk_or, c->nc, M, c->V[c->vcur], ign, c->touched,
-                     c->tail + 2};
+                     c->counters + 2, c->chunk_or, c->nc, M, c->V[c->vcur], ign};
   a.fx = FixArgs{c->cur_traces, c->cur_stride, n, c->skip, c->fix_list, c->counters + 3,
                  c->chunk_or, c->chunk_cls, c->cur_chunks, c->cur_seg_len, c->flags, c->tflags,
                  c->nfw};
@@ -3759,9 +3794,7 @@ int fused_tail(kbz_ctx *c, uint8_t *hnb_out, hipStream_t s) {
   a.nfw = c->nfw;
   a.listed = dr ? c->flags : nullptr;
   a.win_items = c->win_items;
-  a.hnb_out = hnb_out;
   a.tail = c->tail;
-  a.err_out = c->d_err;
   a.shard_last = c->shard_last;
   a.neq = c->neq;
   a.bad_list = c->bad_list;
@@ -3773,9 +3806,28 @@ int fused_tail(kbz_ctx *c, uint8_t *hnb_out, hipStream_t s) {
   a.fix_cnt_w = c->counters + 3;
   hipEvent_t st0;
   if (stage_begin(c, s, &st0)) return -1;
-  hipLaunchKernelGGL(k_tail, dim3(cdiv(M / 16, 256), c->cur_nseg, c->nc), dim3(256), 0, s, a);
+  const unsigned ncg = cdiv(M / 16, 256);
+  hipLaunchKernelGGL(k_tail, dim3(ncg, c->cur_nseg, c->nc), dim3(256), 0, s, a);
   HIP_TRY(hipGetLastError());
   if (stage_end(c, s, KBZ_STAGE_SCAN, st0)) return -1;
+  FinArgs f{};
+  f.ra = a.ra;
+  f.items = c->items;
+  f.cap = c->item_cap;
+  f.counters = c->counters;
+  f.tail = c->tail;
+  f.tail_fix_words = ncg;
+  f.hnb_out = hnb_out;
+  f.err_out = c->d_err;
+  f.shard_last = c->shard_last;
+  f.flags_w = c->flags;
+  f.fix_list_w = c->fix_list;
+  f.fix_cnt = dr ? c->counters + 3 : nullptr;
+  f.nchunks = c->cur_chunks;
+  if (stage_begin(c, s, &st0)) return -1;
+  hipLaunchKernelGGL(k_fin, dim3(512), dim3(256), 0, s, f);
+  HIP_TRY(hipGetLastError());
+  if (stage_end(c, s, KBZ_STAGE_RESOLVE, st0)) return -1;
   std::swap(c->segor, c->segor_alt);
   c->vcur = vn;
   c->stage = 0;
@@ -3939,7 +3991,7 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
                      c->mode == KBZ_MODE_DYNAMORIO ? c->flags : nullptr, c->win_items,
                      ClaimArgs{c->cur_traces, c->cur_stride, (uint32_t)c->cur_n, c->mode,
                                c->cur_outcome, c->mode == KBZ_MODE_DYNAMORIO ? c->skip : nullptr,
-                               c->hnb32, c->counters + 2, nullptr, nullptr});
+                               c->hnb32, c->counters + 2});
   HIP_TRY(hipGetLastError());
   if (stage_end(c, s, KBZ_STAGE_SCAN, st0)) return -1;
   if (c->cur_n) {
@@ -3948,7 +4000,7 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
                        ResolveArgs{c->cur_traces, c->cur_stride, (uint32_t)c->cur_n, c->mode,
                                    c->cur_outcome, c->mode == KBZ_MODE_DYNAMORIO ? c->skip : nullptr,
                                    c->hnb32, c->counters + 2, c->chunk_or, c->nc, (uint32_t)c->M,
-                                   c->V[c->vcur], ign, nullptr, nullptr},
+                                   c->V[c->vcur], ign},
                        c->items, c->counters, c->item_cap);
     HIP_TRY(hipGetLastError());
     if (stage_end(c, s, KBZ_STAGE_RESOLVE, st0)) return -1;
@@ -3992,7 +4044,7 @@ int kbz_triage_batch_device(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_
     return 0;
   }
   if (c && c->fused_ok && n && c->stage == 0) {  // one shard: pass 1, [k_skip], k_tail
-    if (shard_begin_impl(c, traces, n, stride, outcome, h32_out, x64_out, want, stream, hnb_out,
+    if (shard_begin_impl(c, traces, n, stride, outcome, h32_out, x64_out, want, stream, nullptr,
                          true))
       return -1;
     DevGuard g(c->device);
@@ -4055,7 +4107,12 @@ int kbz_sync(kbz_ctx_t *c, void *stream) {
   if (cnt[1] || cnt[2]) {  // sticky until reported here
     HIP_TRY(hipMemset(c->counters + 1, 0, 2 * sizeof(uint32_t)));
     c->h_err[0] = c->h_err[1] = 0;  // k_pack's host-mapped copy: reported now, not again
-    return fail(cnt[1] ? "claim list overflow" : "inconsistent claim (internal error)");
+    // the inconsistency flags name the site: 2 inline claim (k_scan / k_tail), 8 window item,
+    // 16 byte item, 4 / 64 an item never written (k_tail helper / last workgroup), 32 a fix-path
+    // flag never set (k_tail)
+    char msg[96];
+    snprintf(msg, sizeof msg, "inconsistent claim (internal error, flags 0x%x)", cnt[2]);
+    return fail(cnt[1] ? "claim list overflow" : msg);
   }
   c->h_err[0] = c->h_err[1] = 0;
   return 0;

@@ -28,11 +28,19 @@ torch.cuda.synchronize()
 buf = np.zeros(4096 * 2 * 4, np.uint64)
 f(buf.ctypes.data_as(C.c_void_p), buf.size)
 st = buf.reshape(-1, 16, 4)[:256].astype(np.float64)  # [chunk][wave][phase]
-names = (["p0", "p1", "p2", "p3"] if os.environ.get("KBZ_STAMP_NAMES") == "d"
-         else ["work|xform", "barrier", "vmcnt|reads", "fill|finish"])
+D_NAMES = {"C": ["chain", "ready wait", "LDS read wait", "flag read"],
+           "N": ["compare", "ready wait", "LDS read wait", "-"],
+           "X": ["vmcnt wait", "classify+OR", "freed wait", "mix+ring+stores+loads"]}
+dmode = os.environ.get("KBZ_STAMP_NAMES") == "d"
 for w in range(16):
     tot = st[:, w, :].sum(axis=1)
     if np.median(tot) == 0:
         continue
-    cols = "  ".join(f"{nm} {np.median(st[:, w, i]) / 1e6:7.3f}M" for i, nm in enumerate(names))
-    print(f"wave {w:2d}: total {np.median(tot) / 1e6:7.3f}M cycles  {cols}")
+    if dmode:
+        kind = "C" if w == 0 else "N" if w == 4 else "X"
+        names = D_NAMES[kind]
+    else:
+        kind, names = "", ["work|xform", "barrier", "vmcnt|reads", "fill|finish"]
+    cols = "  ".join(f"{nm} {np.median(st[:, w, i]) / 1e6:7.3f}M ({100 * np.median(st[:, w, i] / tot):4.1f}%)"
+                     for i, nm in enumerate(names))
+    print(f"wave {w:2d} {kind}: total {np.median(tot) / 1e6:7.3f}M cycles  {cols}")
