@@ -2511,6 +2511,9 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
   const uint32_t col = live ? col0 : 0;
   const size_t kc = (size_t)k * M + col;
   __shared__ int sh_flag;
+  KBZ_TAIL_DECL;
+  const uint32_t tail_id = ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6);
+  (void)tail_id;
   // the next batch's segment ORs start at zero (every segment of this column slice and class)
   if (live)
     for (uint32_t ss = s; ss < kMaxSeg; ss += a.nseg)
@@ -2618,6 +2621,7 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
     ClaimQ cq{claim_q[threadIdx.x >> 6], 0};
     const uint32_t seg_new = (send.x & vr.x & ~prev.x) | (send.y & vr.y & ~prev.y) |
                              (send.z & vr.z & ~prev.z) | (send.w & vr.w & ~prev.w);
+    KBZ_TAIL_MARK();
     if (__ballot(seg_new != 0)) {  // wave-uniform
       for (uint32_t cg = c0; cg < c1; cg += 64) {
         const uint32_t cl = cg + lane;
@@ -2629,6 +2633,7 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
                 ((a.tflags[((size_t)cl * a.nclass + k) * a.nfw + (t0 >> 6)] >> (t0 & 63)) & 0xFull);
         }
         uint64_t mask = __ballot(any);
+        KBZ_TAIL_ADD(walk, (uint32_t)__popcll(mask));
         while (mask) {
           uint32_t cs[KBZ_SCAN_ILP];
 #pragma unroll
@@ -2652,12 +2657,16 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
             const uint4 nb = make_uint4(o[u].x & vr.x & ~prev.x, o[u].y & vr.y & ~prev.y,
                                         o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
             if (__ballot(nb.x | nb.y | nb.z | nb.w)) {
-              if (wave_claimed_bytes(nb) < a.win_items)
+              const uint32_t ncl = wave_claimed_bytes(nb);
+              if (ncl < a.win_items) {
+                KBZ_TAIL_ADD(claims, ncl);
                 claims_enqueue(a.ca, k, cq, c, col, nb, vir, prev);
-              else
+              } else {
+                KBZ_TAIL_ADD(win, 1);
                 emit_items_wave(c, k, col, nb, vir, prev, stg, a.items, a.cap, a.counters,
                                 (uint8_t *)a.chunk_or + (size_t)c * a.nclass * M + kc, live,
                                 a.win_items);
+              }
             }
             prev = or4(prev, o[u]);
           }
@@ -2667,6 +2676,7 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
       flush_items(stg, a.items, a.cap, a.counters);
     }
   }
+  KBZ_TAIL_END(tail_id);
   // Window and byte items are resolved by k_fin, the next launch: helping with them here, while
   // other workgroups still scan, read stale column windows on gfx950 (the running OR a window
   // item leaves over its chunk's column window, stored sc1 and drained before the item was
@@ -2677,7 +2687,8 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
 // The second launch of the fused tail.  Scores are fire-and-forget atomicMax into hnb32 (k_tail's
 // inline claims, then these items); the outputs are copied once every score is final:
 //   - no claim items (the common case: fresh batches on a warm map, every claim inline): k_tail
-//     was the previous launch, so every workgroup copies its slice of the rows at once;
+//     was the previous launch, so every workgroup copies its slice of the rows at once, and
+//     workgroup 0 re-arms the per-batch words (no other workgroup reads them: no ticket);
 //   - otherwise the items are resolved over the whole grid (k_resolve's work) and the LAST
 //     workgroup (an agent-scope ticket after each workgroup's drained atomics) copies all rows
 //     with sc1 loads (k_pack's role).
@@ -2721,36 +2732,9 @@ __device__ __forceinline__ void fin_copy_rows(const FinArgs &a, uint32_t j0, uin
     }
   }
 }
-__global__ __launch_bounds__(256) void k_fin(FinArgs a) {
-  __shared__ int last;
-  const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t wave = gtid >> 6;
-  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-  const uint32_t cnt = min(a.counters[0], a.cap);  // k_tail's appends: an earlier launch
-  if (cnt == 0) {
-    fin_copy_rows(a, 4 * gtid, 4 * gridDim.x * blockDim.x, false);
-  } else {
-    for (uint32_t it = wave; it < cnt; it += nwaves) {
-      const uint64_t item = a.items[it];
-      if (!item) {  // reserved and never written
-        if ((threadIdx.x & 63) == 0) atomicOr(a.ra.err, 64u);
-        continue;
-      }
-      resolve_item(a.ra, item);
-      if ((threadIdx.x & 63) == 0) a.items[it] = 0;  // the list is all-zero between batches
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics and stores are done
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(&a.tail[0], 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  if (cnt) fin_copy_rows(a, 4 * threadIdx.x, 4 * blockDim.x, true);
+// fix-list flags, k_tail's fix-done flags, the sticky error flags' host-mapped copy, the stats
+// words and the per-batch counters (one workgroup)
+__device__ __forceinline__ void fin_rearm(const FinArgs &a) {
   const uint32_t nfix = a.fix_cnt ? min(ld_sc1(a.fix_cnt), a.nchunks) : 0u;
   for (uint32_t i = threadIdx.x; i < nfix; i += blockDim.x) a.flags_w[a.fix_list_w[i]] = 0;
   for (uint32_t i = threadIdx.x; i < a.tail_fix_words; i += blockDim.x) a.tail[kTailFixDone + i] = 0;
@@ -2766,6 +2750,39 @@ __global__ __launch_bounds__(256) void k_fin(FinArgs a) {
     a.shard_last[0] = a.shard_last[1] = 0;
     for (int i = 0; i < 6; i++) a.tail[i] = 0;
   }
+}
+__global__ __launch_bounds__(256) void k_fin(FinArgs a) {
+  __shared__ int last;
+  const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t wave = gtid >> 6;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t cnt = min(a.counters[0], a.cap);  // k_tail's appends: an earlier launch
+  if (cnt == 0) {
+    fin_copy_rows(a, 4 * gtid, 4 * gridDim.x * blockDim.x, false);
+    if (blockIdx.x == 0) fin_rearm(a);
+    return;
+  }
+  for (uint32_t it = wave; it < cnt; it += nwaves) {
+    const uint64_t item = a.items[it];
+    if (!item) {  // reserved and never written
+      if ((threadIdx.x & 63) == 0) atomicOr(a.ra.err, 64u);
+      continue;
+    }
+    resolve_item(a.ra, item);
+    if ((threadIdx.x & 63) == 0) a.items[it] = 0;  // the list is all-zero between batches
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics and stores are done
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(&a.tail[0], 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  fin_copy_rows(a, 4 * threadIdx.x, 4 * blockDim.x, true);
+  fin_rearm(a);
 }
 
 // ---------------------------------------------------------------------------------------------

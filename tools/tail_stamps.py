@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""k_scan per-wave records of a KBZ_TAIL_STAMPS build (diagnostic only, never for results):
+"""k_scan / k_tail per-wave records of a KBZ_TAIL_STAMPS build (diagnostic only, never for results):
 config-2 fresh batches (bench.py's generator, DynamoRIO), then, per batch, the distribution of
 wave durations in k_scan, the prologue share, and the work of the slowest waves (chunks walked,
 inline claims, window items).
