@@ -113,6 +113,18 @@ __device__ __forceinline__ uint64_t h32_step_fast(uint64_t h, uint64_t k) {
   asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(t), "s"(c));
   return r;
 }
+// The inverse of h32_mix (a bijection of 64-bit words: both constants are odd), so pass 1 can
+// read a transformed word back from the mixed words it leaves in LDS for the chain.
+constexpr uint64_t inv_odd64(uint64_t c) {  // c^-1 mod 2^64 (Newton: 5 doublings of 3 bits)
+  uint64_t x = c;
+  for (int i = 0; i < 5; i++) x *= 2 - c * x;
+  return x;
+}
+constexpr uint64_t kH32C1Inv = inv_odd64(kH32C1), kH32C2Inv = inv_odd64(kH32C2);
+static_assert(kH32C1 * kH32C1Inv == 1 && kH32C2 * kH32C2Inv == 1, "h32_mix inverse");
+__device__ __forceinline__ uint64_t h32_unmix(uint64_t k) {
+  return rotl64(k * kH32C2Inv, 33) * kH32C1Inv;
+}
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() is also a release fence for
 // global memory: with vmcnt counting loads and stores in issue order, it drains this wave's
@@ -344,8 +356,23 @@ struct Pass1Args {
   const uint8_t *vcur;  // [3][map_size] virgin maps at batch entry
   uint64_t *tflags;     // [chunks][nclass][nfw]: bit t%64 of word t/64 = tile t of chunk_or stored
   uint32_t nfw;         // flag words per (chunk, class) = ceil(tiles / 64)
-  uint8_t *hnb_clear;   // [n] or null: zeroed here (the fused tail writes only rows it scores)
+  uint8_t *hnb_clear;   // [n] or null: zeroed here
+  uint64_t *frec;       // [chunks][map_size] claim records (k_pass1s DynamoRIO without ignore
+                        // bytes / XXH64, one-shard batches) or null
+  uint64_t *rflags;     // [chunks][nfw]: bit t%64 of word t/64 = tile t's records written
+  uint32_t epoch;       // this batch's record tag (1..1023)
 };
+#ifndef KBZ_REC_MAX_WORDS  // a stored tile with more words holding still-virgin bits gets no
+#define KBZ_REC_MAX_WORDS 4  // records (novelty-heavy batches): its claims read the rows
+#endif
+// Claim record of one still-virgin byte of one chunk (pass 1, stored tiles only): for each bit t
+// of the byte that is still virgin at batch entry, the first row of the chunk holding it (bits
+// 6t..6t+5), the first row whose byte is nonzero (48..53), the batch tag (54..63).  A claim of
+// the tail then needs one 8-B load instead of that byte of all 64 rows (DynamoRIO, chunks off
+// the fix list: a skipped row repeats an earlier row's bytes, so the first holder of a bit is
+// never one, see k_tail).
+constexpr int kRecEpochShift = 54;
+constexpr uint32_t kRecEpochMask = 1023;
 
 // ---------------------------------------------------------------------------------------------
 // pass 1: two waves per 64-trace chunk (lane = trace) sharing two 16-KiB LDS tile buffers.
@@ -381,6 +408,8 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   constexpr bool TMIX = !X64 && (KBZ_PASS1_TMIX == 2 ||
                                  (KBZ_PASS1_TMIX >= 1 && MODE == KBZ_MODE_AFL) ||
                                  (KBZ_PASS1_TMIX == 3 && MODE == KBZ_MODE_DYNAMORIO));
+  // claim records (a.frec): DynamoRIO with the mix in LDS and every byte examined
+  constexpr bool REC = TMIX && MODE == KBZ_MODE_DYNAMORIO && !IGN;
   // AFL modes: the simplified classes' column ORs come from their rows, once per tile
   constexpr bool SROWS = KBZ_PASS1_SROWS && NC > 1;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = 8;  // 8 x 1-KiB loads per wave per tile
@@ -570,7 +599,40 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
     uint64_t tfl[NC];  // stored-tile bits of the current 64-tile flag word
 #pragma unroll
     for (int k = 0; k < NC; k++) tfl[k] = 0;
+    uint64_t rfl = 0;  // records-written bits of the current 64-tile flag word
     uint64_t *tfbase = a.tflags + (size_t)chunk * NC * a.nfw;
+    // claim records of a stored tile (rare on a warm map): the words with still-virgin bits are
+    // read back from the tile buffer (mixed for wave L, which chains it next step) and unmixed
+    auto tile_records = [&](uint32_t s, int b, uint64_t m) {
+      const uint4 *rw = &lds[b * TILE + lane * SLOTS];
+      const int sw = lane & 15;
+      uint64_t wm = __ballot(lane < TW / 8 && m != 0);
+      if (__popcll(wm) > KBZ_REC_MAX_WORDS) return false;
+      uint64_t *fr = a.frec + (size_t)chunk * a.map_size + (size_t)s * TW;
+      const uint64_t ep = (uint64_t)a.epoch << kRecEpochShift;
+      while (wm) {  // wave-uniform
+        const int wi = __builtin_ctzll(wm);
+        wm &= wm - 1;
+        const uint64_t mw = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(m >> 32), wi) << 32) |
+                            __builtin_amdgcn_readlane((uint32_t)m, wi);
+        const uint64_t kq = ((const uint64_t *)&rw[(wi >> 1) ^ sw])[wi & 1];
+        const uint64_t tw = valid ? h32_unmix(kq) : 0ull;
+        for (int bb = 0; bb < 8; bb++) {
+          const uint32_t mb = (uint32_t)(mw >> (8 * bb)) & 0xffu;
+          if (!mb) continue;  // uniform
+          const uint32_t byte = (uint32_t)(tw >> (8 * bb)) & 0xffu;
+          const uint64_t nz = __ballot(byte != 0);
+          uint64_t rec = ep | ((uint64_t)(nz ? __builtin_ctzll(nz) : 63) << 48);
+          for (int t = 0; t < 8; t++) {
+            if (!((mb >> t) & 1)) continue;
+            const uint64_t bm = __ballot((byte >> t) & 1);
+            rec |= (uint64_t)(bm ? __builtin_ctzll(bm) : 63) << (6 * t);
+          }
+          if (lane == 0) fr[wi * 8 + bb] = rec;
+        }
+      }
+      return true;
+    };
     auto transform_tile = [&](uint32_t s, auto rwc) {
       constexpr bool RW = decltype(rwc)::value;  // simplified classes ORed row-wise (few rows)
       const int b = s & 1;
@@ -657,6 +719,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         if (__ballot(lane < TW / 8 && m != 0)) {
           tfl[k] |= 1ull << (s & 63);
           if (lane < TW / 8) *(uint64_t *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) = m;
+          if (REC && a.frec && tile_records(s, b, m)) rfl |= 1ull << (s & 63);
         }
         // segment aggregate, restricted to still-virgin bits like chunk_or (its consumers only
         // use it under & V: k_scan's segment test and V' = V & ~total): almost never an atomic
@@ -666,6 +729,10 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         if ((s & 63) == 63 || s + 1 == ntiles) {
           if (lane == 0) tfbase[k * a.nfw + (s >> 6)] = tfl[k];
           tfl[k] = 0;
+          if (REC && a.frec) {
+            if (lane == 0) a.rflags[(size_t)chunk * a.nfw + (s >> 6)] = rfl;
+            rfl = 0;
+          }
         }
       }
     };
@@ -2061,14 +2128,13 @@ __device__ __forceinline__ uint32_t pick4(uint4 v, int i) {  // i wave-uniform
 // a nonzero byte there -- k_resolve's per-item rule, without the item.
 constexpr int kClaimQ = 8;
 struct ClaimQ {
-  uint4 *q;  // this wave's kClaimQ entries in LDS: {chunk, column, new bits | f2 << 8, 0}
+  uint4 *q;  // this wave's kClaimQ entries in LDS: {chunk, column, new bits | f2 << 8, class}
   int m;     // wave-uniform fill
 };
-__device__ __forceinline__ void claims_flush(const ClaimArgs &ca, int k, ClaimQ &cq) {
+__device__ __forceinline__ void claims_flush(const ClaimArgs &ca, ClaimQ &cq) {
   if (!cq.m) return;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // lane 0's entries are written
   const int lane = threadIdx.x & 63;
-  const int xf = class_xf(ca.mode, k);
   uint4 e[kClaimQ];
   uint32_t raw[kClaimQ];
   int oc[kClaimQ];
@@ -2086,9 +2152,10 @@ __device__ __forceinline__ void claims_flush(const ClaimArgs &ca, int k, ClaimQ 
   for (int j = 0; j < kClaimQ; j++) {
     if (j >= cq.m) break;  // wave-uniform
     const uint64_t row = (uint64_t)e[j].x * kChunk + lane;
+    const int k = (int)e[j].w;  // the entry's class
     const bool ok = row < ca.n && class_of(ca.mode, oc[j]) == k && !sk[j];
     const uint32_t nbits = e[j].z & 0xffu;
-    const uint32_t tb = ok ? byte_xform(raw[j], xf) : 0u;
+    const uint32_t tb = ok ? byte_xform(raw[j], class_xf(ca.mode, k)) : 0u;
     const uint64_t first_nz = __ballot(tb != 0);
     uint64_t claimers = 0;
     for (int bit = 0; bit < 8; bit++) {
@@ -2126,11 +2193,11 @@ __device__ __forceinline__ void claims_enqueue(const ClaimArgs &ca, int k, Claim
     const uint32_t vb = (__builtin_amdgcn_readlane(pick4(vir, wi), L) >> sh) & 0xffu;
     const uint32_t pb = (__builtin_amdgcn_readlane(pick4(prev, wi), L) >> sh) & 0xffu;
     const uint32_t cc = __builtin_amdgcn_readlane(col, L) + b;
-    if (lane == 0) cq.q[cq.m] = make_uint4(chunk, cc, nbits | ((vb == 0xffu && pb == 0) ? 0x100u : 0u), 0);
+    if (lane == 0) cq.q[cq.m] = make_uint4(chunk, cc, nbits | ((vb == 0xffu && pb == 0) ? 0x100u : 0u), (uint32_t)k);
     cq.m++;
     if (lane == L) rem &= ~(1u << b);
     if (r == (1u << b)) lanes &= lanes - 1;
-    if (cq.m == kClaimQ) claims_flush(ca, k, cq);
+    if (cq.m == kClaimQ) claims_flush(ca, cq);
   }
 }
 // number of claimed (nonzero) bytes over the wave: 16 per lane at most, 5 ballots
@@ -2276,7 +2343,7 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
       }
     }
   }
-  claims_flush(ca, k, cq);
+  claims_flush(ca, cq);
   flush_items(stg, items, cap, counters);
   KBZ_TAIL_END(tail_id);
 }
@@ -2491,6 +2558,9 @@ struct TailArgs {
   uint32_t win_items;
   uint32_t *tail;
   uint32_t *shard_last;
+  const uint64_t *frec;    // pass 1's claim records (null: none this batch)
+  const uint64_t *rflags;  // which tiles have them
+  uint32_t epoch;
   // DynamoRIO chain bookkeeping of k_chain (one shard)
   const uint8_t *neq;
   const uint32_t *bad_list;
@@ -2499,6 +2569,48 @@ struct TailArgs {
   uint32_t *saved_ok;
   uint32_t *flags_w, *fix_list_w, *fix_cnt_w;  // the walks' fix list (DynamoRIO)
 };
+#ifndef KBZ_TAIL_INLINE  // 1: k_tail resolves claims of < win_items bytes itself, as k_scan does;
+#define KBZ_TAIL_INLINE 1  // 0: every claim is an item, resolved by k_fin over the whole grid
+#endif                     // (config 2 tail 64 -> 115 us: the 64-row byte reads are the cost)
+// Claims from pass 1's records (a.frec: DynamoRIO, chunk not on the fix list): per lane, each
+// claimed byte of its 16 costs one 8-B load; per new bit its first holder scores 1, or 2 where
+// the byte was all-virgin, nothing earlier had it and that holder is the first nonzero row.  A
+// skipped row is never a first holder: off the fix list it repeats its predecessor's examined
+// bytes (k_skip's link rows), whose chain starts at an applied row of this chunk or at a row
+// whose bytes are already in prev (an earlier chunk) or V (an earlier batch).
+__device__ __forceinline__ void claims_records(const uint64_t *frec, uint32_t epoch, uint32_t chunk,
+                                               uint32_t map_size, uint32_t col, bool live,
+                                               uint4 nb, uint4 vir, uint4 prev, uint32_t *hnb32,
+                                               uint32_t *err) {
+  const uint32_t w[4] = {nb.x, nb.y, nb.z, nb.w};
+  const uint32_t vv[4] = {vir.x, vir.y, vir.z, vir.w};
+  const uint32_t pv[4] = {prev.x, prev.y, prev.z, prev.w};
+  const uint64_t *fr = frec + (size_t)chunk * map_size + col;
+  uint64_t rv[16];
+#pragma unroll
+  for (int b = 0; b < 16; b++) {
+    const uint32_t x = (w[b >> 2] >> (8 * (b & 3))) & 0xffu;
+    rv[b] = (live && x) ? fr[b] : 0ull;
+  }
+#pragma unroll
+  for (int b = 0; b < 16; b++) {
+    const uint32_t x = (w[b >> 2] >> (8 * (b & 3))) & 0xffu;
+    if (!live || !x) continue;
+    const uint64_t rec = rv[b];
+    if ((uint32_t)(rec >> kRecEpochShift) != epoch) {  // no record of this batch: internal error
+      atomicOr(err, 128u);
+      continue;
+    }
+    const bool f2 = ((vv[b >> 2] >> (8 * (b & 3))) & 0xffu) == 0xffu &&
+                    ((pv[b >> 2] >> (8 * (b & 3))) & 0xffu) == 0u;
+    const uint32_t fz = (uint32_t)(rec >> 48) & 63u;
+    for (uint32_t bits = x; bits; bits &= bits - 1) {
+      const int t = __builtin_ctz(bits);
+      const uint32_t r = (uint32_t)(rec >> (6 * t)) & 63u;
+      atomicMax(&hnb32[(size_t)chunk * kChunk + r], (f2 && r == fz) ? 2u : 1u);
+    }
+  }
+}
 __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t bx = blockIdx.x, s = blockIdx.y;
@@ -2654,11 +2766,26 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
             const uint32_t c = cs[u];  // uniform across the wave
             if (c == ~0u) break;
             if (!st[u]) o[u] = make_uint4(0, 0, 0, 0);
-            const uint4 nb = make_uint4(o[u].x & vr.x & ~prev.x, o[u].y & vr.y & ~prev.y,
-                                        o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
+            uint4 nb = make_uint4(o[u].x & vr.x & ~prev.x, o[u].y & vr.y & ~prev.y,
+                                  o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
             if (__ballot(nb.x | nb.y | nb.z | nb.w)) {
-              const uint32_t ncl = wave_claimed_bytes(nb);
-              if (ncl < a.win_items) {
+              if (a.frec && !(a.listed && a.listed[c])) {  // c wave-uniform
+                const uint32_t tl = col / kTileW;  // this lane's tile
+                uint4 nbr = make_uint4(0, 0, 0, 0);  // its claimed bytes with records
+                if ((a.rflags[(size_t)c * a.nfw + (tl >> 6)] >> (tl & 63)) & 1) {
+                  nbr = nb;
+                  nb = make_uint4(0, 0, 0, 0);
+                }
+                if (__ballot(nbr.x | nbr.y | nbr.z | nbr.w)) {
+                  KBZ_TAIL_ADD(claims, wave_claimed_bytes(nbr));
+                  claims_records(a.frec, a.epoch, c, M, col, live, nbr, vir, prev, a.ca.hnb32,
+                                 a.ca.err);
+                }
+              }
+              const uint32_t ncl = wave_claimed_bytes(nb);  // the rest: read the rows
+              if (!__ballot(nb.x | nb.y | nb.z | nb.w)) {
+                // every claimed byte had a record
+              } else if (KBZ_TAIL_INLINE && ncl < a.win_items) {
                 KBZ_TAIL_ADD(claims, ncl);
                 claims_enqueue(a.ca, k, cq, c, col, nb, vir, prev);
               } else {
@@ -2672,7 +2799,7 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
           }
         }
       }
-      claims_flush(a.ca, k, cq);
+      claims_flush(a.ca, cq);
       flush_items(stg, a.items, a.cap, a.counters);
     }
   }
@@ -2708,18 +2835,45 @@ struct FinArgs {
   const uint32_t *fix_cnt;  // null: AFL modes (no fix list)
   uint32_t nchunks;
 };
-__device__ __forceinline__ void fin_copy_rows(const FinArgs &a, uint32_t j0, uint32_t step, bool sc1) {
-  // 4 rows per thread per step (one 16-B load of hnb32), j0 a multiple of 4
+__device__ __forceinline__ void fin_copy_rows_sc1(const FinArgs &a) {
+  // the last workgroup, after the ticket: hnb32 was scored with atomics in this launch (sc1 loads)
+  // 16 x 4 rows in flight per thread
+  const uint32_t n = a.ra.n;
+  constexpr int U = 16;
+  for (uint32_t j0 = 4 * threadIdx.x; j0 < n; j0 += 4 * U * blockDim.x) {
+    uint32_t h[U][4];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const uint32_t j = j0 + 4 * u * blockDim.x + e;
+        h[u][e] = j < n ? ld_sc1(&a.ra.hnb32[j]) : 0u;
+      }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const uint32_t j = j0 + 4 * u * blockDim.x + e;
+        if (j < n) {
+          a.ra.hnb32[j] = 0;
+          if (a.hnb_out) a.hnb_out[j] = (uint8_t)h[u][e];
+        }
+      }
+  }
+}
+__device__ __forceinline__ void fin_copy_rows(const FinArgs &a, uint32_t j0, uint32_t step) {
+  // no items: hnb32 is final since k_tail (an earlier launch); 4 rows per thread per step (one
+  // 16-B load of hnb32), j0 a multiple of 4
   const uint32_t n = a.ra.n;
   for (uint32_t j = j0; j < n; j += step) {
     uint32_t h[4];
-    if (j + 4 <= n && !sc1) {
+    if (j + 4 <= n) {
       const uint4 v = *(const uint4 *)(a.ra.hnb32 + j);
       h[0] = v.x, h[1] = v.y, h[2] = v.z, h[3] = v.w;
       *(uint4 *)(a.ra.hnb32 + j) = make_uint4(0, 0, 0, 0);
     } else {
       for (int u = 0; u < 4; u++) {
-        h[u] = j + u < n ? (sc1 ? ld_sc1(&a.ra.hnb32[j + u]) : a.ra.hnb32[j + u]) : 0u;
+        h[u] = j + u < n ? a.ra.hnb32[j + u] : 0u;
         if (j + u < n) a.ra.hnb32[j + u] = 0;
       }
     }
@@ -2758,18 +2912,39 @@ __global__ __launch_bounds__(256) void k_fin(FinArgs a) {
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   const uint32_t cnt = min(a.counters[0], a.cap);  // k_tail's appends: an earlier launch
   if (cnt == 0) {
-    fin_copy_rows(a, 4 * gtid, 4 * gridDim.x * blockDim.x, false);
+    fin_copy_rows(a, 4 * gtid, 4 * gridDim.x * blockDim.x);
     if (blockIdx.x == 0) fin_rearm(a);
     return;
   }
-  for (uint32_t it = wave; it < cnt; it += nwaves) {
-    const uint64_t item = a.items[it];
-    if (!item) {  // reserved and never written
-      if ((threadIdx.x & 63) == 0) atomicOr(a.ra.err, 64u);
-      continue;
+  // kClaimQ items per wave per round: byte items go through the claim queue (their rows' bytes
+  // in flight together, as k_scan's inline claims), window items one at a time
+  const int lane = threadIdx.x & 63;
+  __shared__ uint4 fin_q[4][kClaimQ];
+  ClaimQ cq{fin_q[threadIdx.x >> 6], 0};
+  const ClaimArgs ca{a.ra.traces, a.ra.stride, a.ra.n, a.ra.mode, a.ra.outcome, a.ra.skip,
+                     a.ra.hnb32, a.ra.err};
+  for (uint32_t it0 = wave * kClaimQ; it0 < cnt; it0 += nwaves * kClaimQ) {
+    const uint64_t mine = (lane < kClaimQ && it0 + lane < cnt) ? a.items[it0 + lane] : 0ull;
+    if (lane < kClaimQ && it0 + lane < cnt) a.items[it0 + lane] = 0;  // all-zero between batches
+#pragma unroll
+    for (int j = 0; j < kClaimQ; j++) {
+      if (it0 + j >= cnt) break;  // wave-uniform
+      const uint64_t item = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(mine >> 32), j) << 32) |
+                            __builtin_amdgcn_readlane((uint32_t)mine, j);
+      if (!item) {  // reserved and never written
+        if (lane == 0) atomicOr(a.ra.err, 64u);
+        continue;
+      }
+      if ((item & 0xff) == 0) {
+        resolve_item(a.ra, item);  // window item
+      } else {
+        if (lane == 0)
+          cq.q[cq.m] = make_uint4(item_chunk(item), (uint32_t)(item >> 11) & 0xffffff,
+                                  (uint32_t)item & 0x1ff, (uint32_t)(item >> 9) & 3);
+        cq.m++;
+      }
     }
-    resolve_item(a.ra, item);
-    if ((threadIdx.x & 63) == 0) a.items[it] = 0;  // the list is all-zero between batches
+    claims_flush(ca, cq);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics and stores are done
   __syncthreads();
@@ -2781,7 +2956,7 @@ __global__ __launch_bounds__(256) void k_fin(FinArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  fin_copy_rows(a, 4 * threadIdx.x, 4 * blockDim.x, true);
+  fin_copy_rows_sc1(a);
   fin_rearm(a);
 }
 
@@ -3166,6 +3341,11 @@ struct kbz_ctx {
   uint8_t *segor_alt = nullptr;  // the other buffer (the fused tail zeroes it and swaps)
   uint32_t *tail = nullptr;      // k_tail's words (kTailFixDone + column groups)
   bool fused_ok = true;          // one-shard batches through k_tail (KBZ_DEBUG_STAGED=1: staged)
+  bool rec_ok = true;            // pass-1 claim records (KBZ_DEBUG_NO_REC=1: off)
+  uint64_t *frec = nullptr;      // [max_chunks][M] claim records, allocated on first use
+  uint64_t *rflags = nullptr;    // [max_chunks][nfw] tiles with records
+  uint32_t epoch = 0;            // the record tag of the current batch (1..1023)
+  bool cur_rec = false;          // the current batch's pass 1 wrote records
   uint8_t *segprev = nullptr;
   uint8_t *total = nullptr;
   uint64_t *items = nullptr;
@@ -3280,7 +3460,8 @@ void free_ctx(kbz_ctx *c) {
                   c->skip, c->neq, c->h32, c->hnb32, c->segor, c->segor_alt, c->tail,
                   c->segprev, c->total,
                   c->items, c->counters, c->shard_last, c->dslot[0], c->dslot[1],
-                  c->dslot_oc[0], c->dslot_oc[1], c->dres_hnb, c->dres_h32, c->dres_x64};
+                  c->dslot_oc[0], c->dslot_oc[1], c->dres_hnb, c->dres_h32, c->dres_x64, c->frec,
+                  c->rflags};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (int i = 0; i < 2; i++) {
@@ -3513,6 +3694,8 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   if (const char *w = getenv("KBZ_DEBUG_NO_SMALL")) c->small_ok = atoi(w) == 0;
   // tests only: one-shard batches through the staged kernels (k_chain ... k_pack) instead of k_tail
   if (const char *w = getenv("KBZ_DEBUG_STAGED")) c->fused_ok = atoi(w) == 0;
+  // tests only: fused DynamoRIO batches without pass-1 claim records (k_tail reads the rows)
+  if (const char *w = getenv("KBZ_DEBUG_NO_REC")) c->rec_ok = atoi(w) == 0;
   bool ok = !dalloc(&c->V[0], 3 * M) && !dalloc(&c->V[1], 3 * M) && !dalloc(&c->last, 2) &&
             !dalloc(&c->chunk_or, c->max_chunks * nc * M) && !dalloc(&c->chunk_cls, c->max_chunks) &&
             !dalloc(&c->tflags, c->max_chunks * nc * c->nfw) &&
@@ -3714,6 +3897,33 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
   a.tflags = c->tflags;
   a.nfw = c->nfw;
   a.hnb_clear = hnb_clear;
+  a.frec = nullptr;
+  a.rflags = nullptr;
+  a.epoch = 0;
+  c->cur_rec = false;
+  // one-shard DynamoRIO batches through k_pass1s without ignore bytes or XXH64: claim records
+  if (fused && c->rec_ok && c->mode == KBZ_MODE_DYNAMORIO && !c->ignore && !a.x64 &&
+      !pass1_is_wide(c->pass1, c->cur_chunks)) {
+    if (!c->frec) {
+      const size_t bytes = (size_t)c->max_chunks * c->M * sizeof(uint64_t);
+      if (hipMalloc((void **)&c->frec, bytes) != hipSuccess ||
+          hipMalloc((void **)&c->rflags, (size_t)c->max_chunks * c->nfw * sizeof(uint64_t)) !=
+              hipSuccess) {
+        (void)hipGetLastError();
+        if (c->frec) (void)hipFree(c->frec);
+        c->frec = nullptr;
+        c->rflags = nullptr;
+        c->rec_ok = false;  // no room: k_tail reads the rows instead
+      }
+    }
+    if (c->frec) {
+      c->epoch = c->epoch % kRecEpochMask + 1;
+      a.frec = c->frec;
+      a.rflags = c->rflags;
+      a.epoch = c->epoch;
+      c->cur_rec = true;
+    }
+  }
   P1Ev pev;
   if (c->timing) {
     if (c->ev_used_n >= kEvFoldAt && fold_pass1(c)) return -1;
@@ -3812,6 +4022,9 @@ int fused_tail(kbz_ctx *c, uint8_t *hnb_out, hipStream_t s) {
   a.listed = dr ? c->flags : nullptr;
   a.win_items = c->win_items;
   a.tail = c->tail;
+  a.frec = c->cur_rec ? c->frec : nullptr;
+  a.rflags = c->rflags;
+  a.epoch = c->epoch;
   a.shard_last = c->shard_last;
   a.neq = c->neq;
   a.bad_list = c->bad_list;
