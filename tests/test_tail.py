@@ -70,3 +70,30 @@ def test_tail_touched_rows_only(gpu):
         ctx.sync()
         np.testing.assert_array_equal(out["hnb"].cpu().numpy(), exp["hnb"])
         assert set(np.nonzero(exp["hnb"])[0]) <= {17, 1234, 4321}
+
+
+@pytest.mark.parametrize("rec", [True, False], ids=["records", "rows"])
+def test_claim_records_fresh_batches(gpu, rec, monkeypatch):
+    """Pass-1 claim records (k_pass1s, DynamoRIO, hash32 only): a warm map, then fresh batches of
+    the same target (slices of one generated run: one hot set) with repeated execs and a restored
+    last hash (row 0 skipped with an unknown predecessor: its chunk goes to the fix list) -- the
+    records path for tiles with few still-virgin words, the row reads for the rest and for
+    fix-list chunks; against the oracle, and the same batches with records off."""
+    if not rec:
+        monkeypatch.setenv("KBZ_DEBUG_NO_REC", "1")
+    m, n, nb = 16384, 64 * 40 + 17, 6
+    t_all, oc_all = synth.sparse_np(n * nb, m, seed=1401, hot_frac=0.02)
+    with TriageContext(m, MODE_DYNAMORIO, n, pass1="narrow") as ctx:
+        for i in range(nb):
+            t, oc = t_all[i * n:(i + 1) * n].copy(), oc_all[i * n:(i + 1) * n]
+            if i >= 2:
+                t[100:140] = t[99]  # repeats: link rows (skipped, same bytes)
+                t[700:705] = t[700]
+            if i == 4:  # a restored hash equal to row 0's: row 0 and its repeats are recomputed
+                t[1:70] = t[0]
+                ctx.last_hash = int(oracle.triage_batch(MODE_DYNAMORIO, t[:1], None)["h32"][0])
+            e = check(MODE_DYNAMORIO, t, oc, ctx=ctx, want=WANT_H32)
+            if i == 4:
+                assert ctx.stats()["fixed_chunks"] >= 2
+            if i >= 1:
+                assert 0 < (e["hnb"] > 0).sum() < n // 2  # a warm map: some rows are new
