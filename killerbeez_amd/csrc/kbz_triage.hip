@@ -363,8 +363,8 @@ struct Pass1Args {
   uint32_t epoch;       // this batch's record tag (1..1023)
 };
 #ifndef KBZ_REC_MAX_WORDS  // a stored tile with more words holding still-virgin bits gets no
-#define KBZ_REC_MAX_WORDS 4  // records (novelty-heavy batches): its claims read the rows
-#endif
+#define KBZ_REC_MAX_WORDS 2  // records (fresh maps, novelty-heavy batches): its claims read rows
+#endif                       // (one ballot per stored tile; a byte count cost novelty pass 1 +30 %)
 // Claim record of one still-virgin byte of one chunk (pass 1, stored tiles only): for each bit t
 // of the byte that is still virgin at batch entry, the first row of the chunk holding it (bits
 // 6t..6t+5), the first row whose byte is nonzero (48..53), the batch tag (54..63).  A claim of
@@ -2835,12 +2835,22 @@ struct FinArgs {
   const uint32_t *fix_cnt;  // null: AFL modes (no fix list)
   uint32_t nchunks;
 };
-__device__ __forceinline__ void fin_copy_rows_sc1(const FinArgs &a) {
-  // the last workgroup, after the ticket: hnb32 was scored with atomics in this launch (sc1 loads)
-  // 16 x 4 rows in flight per thread
+constexpr uint32_t kFinCopiers = 16;
+__device__ __forceinline__ bool spin_until_ge(const uint32_t *p, uint32_t want) {
+  for (uint32_t it = 0; it < kSpinMax; it++) {
+    if (ld_sc1(p) >= want) return true;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
+__device__ __forceinline__ void fin_copy_rows_sc1(const FinArgs &a, uint32_t part, uint32_t parts) {
+  // the copiers, after every workgroup arrived: hnb32 was scored with atomics in this launch (sc1
+  // loads); copier `part` of `parts` takes every parts-th block of 4 x 16 x blockDim rows, 16 x 4
+  // rows in flight per thread
   const uint32_t n = a.ra.n;
   constexpr int U = 16;
-  for (uint32_t j0 = 4 * threadIdx.x; j0 < n; j0 += 4 * U * blockDim.x) {
+  for (uint32_t j0 = 4 * threadIdx.x + part * 4 * U * blockDim.x; j0 < n;
+       j0 += parts * 4 * U * blockDim.x) {
     uint32_t h[U][4];
 #pragma unroll
     for (int u = 0; u < U; u++)
@@ -2946,9 +2956,26 @@ __global__ __launch_bounds__(256) void k_fin(FinArgs a) {
     }
     claims_flush(ca, cq);
   }
+  // The last kFinCopiers workgroups to arrive copy the rows together once every workgroup has
+  // arrived: they only wait for workgroups that already hold a ticket or are still to be
+  // dispatched (at most kFinCopiers - 1 of them), never for one that waits.  The last copier
+  // to finish re-arms.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics and stores are done
   __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(&a.tail[0], 1u) == gridDim.x - 1;
+  const uint32_t G = gridDim.x, nc = min(G, (uint32_t)kFinCopiers);
+  if (threadIdx.x == 0) {
+    const uint32_t tk = atomicAdd(&a.tail[0], 1u);
+    last = tk >= G - nc ? (int)(tk - (G - nc)) : -1;  // copier index, or -1
+    if (last >= 0 && !spin_until_ge(&a.tail[0], G)) atomicOr(a.ra.err, 64u);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (last < 0) return;
+  fin_copy_rows_sc1(a, (uint32_t)last, nc);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(&a.tail[1], 1u) == nc - 1;  // the last copier done
   __syncthreads();
   if (!last) return;
   if (threadIdx.x == 0) {
@@ -2956,7 +2983,6 @@ __global__ __launch_bounds__(256) void k_fin(FinArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  fin_copy_rows_sc1(a);
   fin_rearm(a);
 }
 
