@@ -2754,12 +2754,15 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
             mask &= mask - 1;
           }
           uint4 o[KBZ_SCAN_ILP];
-          bool st[KBZ_SCAN_ILP];
+          bool st[KBZ_SCAN_ILP], lst[KBZ_SCAN_ILP], rec[KBZ_SCAN_ILP];
+          const uint32_t tl = col / kTileW;  // this lane's tile
 #pragma unroll
-          for (int u = 0; u < KBZ_SCAN_ILP; u++) {
+          for (int u = 0; u < KBZ_SCAN_ILP; u++) {  // every load of the group in one round trip
             const uint32_t c = cs[u] != ~0u ? cs[u] : cs[0];
             o[u] = *(const uint4 *)(a.chunk_or + (size_t)c * a.nclass * M + kc);
-            st[u] = tile_stored(a.tflags, a.nfw, a.nclass, c, k, col) || (a.listed && a.listed[c]);
+            lst[u] = a.listed && a.listed[c];
+            st[u] = tile_stored(a.tflags, a.nfw, a.nclass, c, k, col) || lst[u];
+            rec[u] = a.frec && ((a.rflags[(size_t)c * a.nfw + (tl >> 6)] >> (tl & 63)) & 1);
           }
 #pragma unroll
           for (int u = 0; u < KBZ_SCAN_ILP; u++) {
@@ -2769,10 +2772,9 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
             uint4 nb = make_uint4(o[u].x & vr.x & ~prev.x, o[u].y & vr.y & ~prev.y,
                                   o[u].z & vr.z & ~prev.z, o[u].w & vr.w & ~prev.w);
             if (__ballot(nb.x | nb.y | nb.z | nb.w)) {
-              if (a.frec && !(a.listed && a.listed[c])) {  // c wave-uniform
-                const uint32_t tl = col / kTileW;  // this lane's tile
-                uint4 nbr = make_uint4(0, 0, 0, 0);  // its claimed bytes with records
-                if ((a.rflags[(size_t)c * a.nfw + (tl >> 6)] >> (tl & 63)) & 1) {
+              if (a.frec && !lst[u]) {  // lst wave-uniform
+                uint4 nbr = make_uint4(0, 0, 0, 0);  // this lane's claimed bytes with records
+                if (rec[u]) {
                   nbr = nb;
                   nb = make_uint4(0, 0, 0, 0);
                 }
