@@ -2572,6 +2572,21 @@ struct TailArgs {
 #ifndef KBZ_TAIL_INLINE  // 1: k_tail resolves claims of < win_items bytes itself, as k_scan does;
 #define KBZ_TAIL_INLINE 1  // 0: every claim is an item, resolved by k_fin over the whole grid
 #endif                     // (config 2 tail 64 -> 115 us: the 64-row byte reads are the cost)
+// One claimed byte's record: info = new bits | f2 << 8 (see claims_records).
+__device__ __forceinline__ void record_score(uint64_t rec, uint32_t info, uint32_t chunk,
+                                             uint32_t epoch, uint32_t *hnb32, uint32_t *err) {
+  if ((uint32_t)(rec >> kRecEpochShift) != epoch) {  // no record of this batch: internal error
+    atomicOr(err, 128u);
+    return;
+  }
+  const bool f2 = (info >> 8) & 1;
+  const uint32_t fz = (uint32_t)(rec >> 48) & 63u;
+  for (uint32_t bits = info & 0xffu; bits; bits &= bits - 1) {
+    const int t = __builtin_ctz(bits);
+    const uint32_t r = (uint32_t)(rec >> (6 * t)) & 63u;
+    atomicMax(&hnb32[(size_t)chunk * kChunk + r], (f2 && r == fz) ? 2u : 1u);
+  }
+}
 // Claims from pass 1's records (a.frec: DynamoRIO, chunk not on the fix list): per lane, each
 // claimed byte of its 16 costs one 8-B load; per new bit its first holder scores 1, or 2 where
 // the byte was all-virgin, nothing earlier had it and that holder is the first nonzero row.  A
@@ -2755,6 +2770,10 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
           }
           uint4 o[KBZ_SCAN_ILP];
           bool st[KBZ_SCAN_ILP], lst[KBZ_SCAN_ILP], rec[KBZ_SCAN_ILP];
+          // each chunk's first record claim of this lane: its load is issued in the walk and
+          // scored after the group, so the group's record loads share one round trip
+          uint64_t rv[KBZ_SCAN_ILP];
+          uint32_t ri[KBZ_SCAN_ILP];  // new bits | f2 << 8 | 1 << 16 (pending)
           const uint32_t tl = col / kTileW;  // this lane's tile
 #pragma unroll
           for (int u = 0; u < KBZ_SCAN_ILP; u++) {  // every load of the group in one round trip
@@ -2763,6 +2782,8 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
             lst[u] = a.listed && a.listed[c];
             st[u] = tile_stored(a.tflags, a.nfw, a.nclass, c, k, col) || lst[u];
             rec[u] = a.frec && ((a.rflags[(size_t)c * a.nfw + (tl >> 6)] >> (tl & 63)) & 1);
+            ri[u] = 0;
+            rv[u] = 0;
           }
 #pragma unroll
           for (int u = 0; u < KBZ_SCAN_ILP; u++) {
@@ -2780,8 +2801,25 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
                 }
                 if (__ballot(nbr.x | nbr.y | nbr.z | nbr.w)) {
                   KBZ_TAIL_ADD(claims, wave_claimed_bytes(nbr));
-                  claims_records(a.frec, a.epoch, c, M, col, live, nbr, vir, prev, a.ca.hnb32,
-                                 a.ca.err);
+                  const uint32_t w4[4] = {nbr.x, nbr.y, nbr.z, nbr.w};
+                  int b0 = -1;
+#pragma unroll
+                  for (int b = 15; b >= 0; b--)
+                    if ((w4[b >> 2] >> (8 * (b & 3))) & 0xffu) b0 = b;
+                  if (live && b0 >= 0) {
+                    const int wi = b0 >> 2, sh = 8 * (b0 & 3);
+                    const uint32_t x = (pick4(nbr, wi) >> sh) & 0xffu;
+                    const bool f2 = ((pick4(vir, wi) >> sh) & 0xffu) == 0xffu &&
+                                    ((pick4(prev, wi) >> sh) & 0xffu) == 0u;
+                    ri[u] = x | (f2 ? 0x100u : 0u) | 0x10000u;
+                    rv[u] = a.frec[(size_t)c * M + col + b0];
+                    const uint32_t clr = ~(0xffu << sh);  // the rest of the lane's bytes
+                    nbr = make_uint4(wi == 0 ? nbr.x & clr : nbr.x, wi == 1 ? nbr.y & clr : nbr.y,
+                                     wi == 2 ? nbr.z & clr : nbr.z, wi == 3 ? nbr.w & clr : nbr.w);
+                  }
+                  if (__ballot(nbr.x | nbr.y | nbr.z | nbr.w))  // a lane with more (rare)
+                    claims_records(a.frec, a.epoch, c, M, col, live, nbr, vir, prev, a.ca.hnb32,
+                                   a.ca.err);
                 }
               }
               const uint32_t ncl = wave_claimed_bytes(nb);  // the rest: read the rows
@@ -2799,6 +2837,9 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
             }
             prev = or4(prev, o[u]);
           }
+#pragma unroll
+          for (int u = 0; u < KBZ_SCAN_ILP; u++)
+            if (ri[u] >> 16) record_score(rv[u], ri[u], cs[u], a.epoch, a.ca.hnb32, a.ca.err);
         }
       }
       claims_flush(a.ca, cq);
