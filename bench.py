@@ -35,6 +35,7 @@ import json
 
 import numpy as np
 import os
+import shutil
 import socket
 import subprocess
 import sys
@@ -260,6 +261,23 @@ def cpu_baseline_all_cores(traces_dev, outcome_dev, mode, seconds):
                       f"threads x t(1) / t(threads) of a register-only chain per thread"}
 
 
+# ---- profiler children --------------------------------------------------------------------------
+#
+# Every profiler child (PMC passes, the kernel trace) is started by profile_first() BEFORE this
+# process touches the GPU, and rocprofv3 (a `#!/usr/bin/env python3` script) is started as
+# [sys.executable, rocprofv3] so no `env` hop execs anything.  The children themselves run with
+# --no-pmc --no-ktrace: a profiled child never starts another profiler (round 4's PMC children
+# did: their nested kernel-trace launches were the execs the GPU box refused).
+
+def _rocprof():
+    path = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    return [sys.executable, path]
+
+
+def _child_args():
+    return [os.path.abspath(__file__), "--no-cpu", "--no-variants", "--no-pmc", "--no-ktrace"]
+
+
 # ---- roofline traffic (PMC) --------------------------------------------------------------------
 
 def _pmc_pass(counter, workload_args, outdir, timeout=150, kernel="k_pass1"):
@@ -268,9 +286,8 @@ def _pmc_pass(counter, workload_args, outdir, timeout=150, kernel="k_pass1"):
     import csv
     import glob
 
-    cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir, "-o", "run",
-           "--", sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-variants",
-           "--no-pmc", *workload_args]
+    cmd = [*_rocprof(), "--pmc", counter, "--output-format", "csv", "-d", outdir, "-o", "run",
+           "--", sys.executable, *_child_args(), *workload_args]
     subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=timeout,
                    check=True)
     vals = []
@@ -303,36 +320,22 @@ def live_traffic(args, warmup=1, steps=4):
                       f"{med(write) * 1024:.0f} B"}
 
 
-def live_kernel_trace(args, warmup=3, steps=12):
-    """The roofline's kernel time from the profiler: a rocprofv3 --kernel-trace child run of the
-    same workload (no variants, no PMC); its timed steps' pass-1 dispatches are the last `steps`
-    pass-1 dispatches of the trace.  Returns their average duration (and min / max), the child's
-    own ms_per_step and HIP-event pass-1 time, and every kernel of those steps (start relative to
-    the step's pass 1, duration), also written to $KBZ_BENCH_KTRACE_OUT (a JSON the evidence
-    script commits under profiles/) -- so the line's `frac` can be recomputed from profiles/."""
+def summarize_ktrace(csv_files, steps, kernel_prefix="k_pass1"):
+    """Parse rocprofv3 kernel_trace.csv files of one run: the last `steps` dispatches whose name
+    starts with `kernel_prefix` are its timed steps (runs without variants).  Returns
+    (summary, per-step kernel lists, pass-1 durations in ms) or None."""
     import csv
-    import glob
-    import tempfile
 
-    wa = ["--workload", args.workload, "--mode", args.mode, "--batch", str(args.batch),
-          "--map-size", str(args.map_size), "--warmup", str(warmup), "--steps", str(steps),
-          "--seed", str(args.seed), *(["--hash"] if args.hash else [])]
-    with tempfile.TemporaryDirectory() as d:
-        cmd = ["rocprofv3", "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run",
-               "--", sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-variants",
-               "--no-pmc", "--no-ktrace", *wa]
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, check=True)
-        child = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-        rows = []
-        for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
-            for row in csv.DictReader(open(f)):
-                name = row.get("Kernel_Name", "")
-                if "(anonymous namespace)::k_" not in name:
-                    continue
-                k = name.split("(anonymous namespace)::")[1].split("(")[0].split("<")[0]
-                rows.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), k))
+    rows = []
+    for f in csv_files:
+        for row in csv.DictReader(open(f)):
+            name = row.get("Kernel_Name", "")
+            if "(anonymous namespace)::k_" not in name:
+                continue
+            k = name.split("(anonymous namespace)::")[1].split("(")[0].split("<")[0]
+            rows.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), k))
     rows.sort()
-    p1 = [i for i, x in enumerate(rows) if x[2].startswith("k_pass1")]
+    p1 = [i for i, x in enumerate(rows) if x[2].startswith(kernel_prefix)]
     if len(p1) < steps:
         return None
     first = p1[-steps]
@@ -348,13 +351,40 @@ def live_kernel_trace(args, warmup=3, steps=12):
     span = [(rows[timed[si + 1]][0] - rows[i][0]) / 1e6 for si, i in enumerate(timed[:-1])]
     avg = sum(durs) / len(durs)
     out = {"avg_ms": round(avg, 4), "min_ms": round(min(durs), 4), "max_ms": round(max(durs), 4),
-           "dispatches": len(durs),
-           "child_ms_per_step": child.get("ms_per_step"),
-           "child_hip_event_avg_ms": child.get("roofline", {}).get("avg_launch_ms"),
-           "median_step_span_ms": round(sorted(span)[len(span) // 2], 4) if span else None,
-           "what": f"rocprofv3 --kernel-trace of a child run of this workload ({warmup} warmup + "
-                   f"{steps} timed fresh batches); the last {steps} pass-1 dispatches = its timed "
-                   "steps; step span = pass-1 start to the next pass-1 start"}
+           "median_ms": round(sorted(durs)[len(durs) // 2], 4), "dispatches": len(durs),
+           "median_step_span_ms": round(sorted(span)[len(span) // 2], 4) if span else None}
+    return out, per_step, durs
+
+
+def live_kernel_trace(args, warmup=3, steps=12):
+    """The roofline's kernel time from the profiler: a rocprofv3 --kernel-trace child run of the
+    same workload (no variants, no PMC); its timed steps' pass-1 dispatches are the last `steps`
+    pass-1 dispatches of the trace.  Returns their average duration (and min / max), the child's
+    own ms_per_step and HIP-event pass-1 time, and every kernel of those steps (start relative to
+    the step's pass 1, duration), also written to $KBZ_BENCH_KTRACE_OUT (a JSON the evidence
+    script commits under profiles/) -- so the line's `frac` can be recomputed from profiles/."""
+    import glob
+    import tempfile
+
+    wa = ["--workload", args.workload, "--mode", args.mode, "--batch", str(args.batch),
+          "--map-size", str(args.map_size), "--warmup", str(warmup), "--steps", str(steps),
+          "--seed", str(args.seed), *(["--hash"] if args.hash else [])]
+    with tempfile.TemporaryDirectory() as d:
+        cmd = [*_rocprof(), "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run",
+               "--", sys.executable, *_child_args(), *wa]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, check=True)
+        child = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+        got = summarize_ktrace(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"),
+                                         recursive=True), steps)
+    if got is None:
+        return None
+    out, per_step, durs = got
+    out.update({"child_ms_per_step": child.get("ms_per_step"),
+                "child_hip_event_avg_ms": child.get("roofline", {}).get("avg_launch_ms"),
+                "what": f"rocprofv3 --kernel-trace of a child run of this workload ({warmup} "
+                        f"warmup + {steps} timed fresh batches), started before this process "
+                        f"touched the GPU; the last {steps} pass-1 dispatches = its timed steps; "
+                        "step span = pass-1 start to the next pass-1 start"})
     dest = os.environ.get("KBZ_BENCH_KTRACE_OUT")
     if dest:
         os.makedirs(os.path.dirname(os.path.abspath(dest)), exist_ok=True)
@@ -509,7 +539,7 @@ def novelty_heavy(args, mode, want, batches, dev, steps=5):
                     "steps), own warmed-up context"}
 
 
-def main_triage(args):
+def main_triage(args, pre):
     import torch
 
     from killerbeez_amd import synth
@@ -610,27 +640,10 @@ def main_triage(args):
             variants["afl_all_crash_simplify"] = crash_variant(args, pool, barrier_sync, dev)
             variants["novelty_heavy"] = novelty_heavy(args, mode, want, fresh, dev)
     del pool, fresh
-    torch.cuda.empty_cache()  # the PMC child run below allocates its own batches
-    traffic = None
-    if rank == 0 and world == 1 and args.pmc:
-        try:
-            traffic = live_traffic(args)
-        except Exception as e:  # noqa: BLE001 -- reported, never fatal
-            traffic = {"bytes": None, "source": f"live PMC failed: {type(e).__name__}"}
+    traffic = pre["traffic"]
     if traffic is None:
         traffic = stored_traffic(args.workload) or {"bytes": None, "source": "none"}
-    ktrace = None
-    if rank == 0 and world == 1 and args.ktrace:
-        try:
-            ktrace = live_kernel_trace(args, steps=min(args.steps, 12))
-        except Exception as e:  # noqa: BLE001 -- reported, never fatal
-            ktrace = {"avg_ms": None, "what": f"kernel trace failed: {type(e).__name__}: {e}"[:300]}
-    valu = None
-    if rank == 0 and world == 1 and args.pmc and dense:
-        try:
-            valu = live_valu(args)
-        except Exception as e:  # noqa: BLE001 -- reported, never fatal
-            valu = {"instructions_per_launch": None, "what": f"live PMC failed: {type(e).__name__}"}
+    ktrace, valu = pre["ktrace"], pre["valu"]
     wide = B < 512 * 64
     if mode == MODES["dynamorio"]:
         kname = "k_pass1d" if wide else "k_pass1s"
@@ -712,7 +725,7 @@ def main_triage(args):
 
 # ---- config 4: merger --------------------------------------------------------------------------
 
-def main_merge(args):
+def main_merge(args, pre):
     """BASELINE config 4: N client states (3 virgin maps of 64 KiB each) AND-folded into one
     (merger/merger.c:79-99), states resident in HBM, split evenly over the ranks (strong
     scaling: the N states are the job); one step = one fold of all N (local fold, all-gather of
@@ -781,15 +794,9 @@ def main_merge(args):
                         "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": bytes_}}
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = merge_cpu_baseline(states, args.cpu_seconds)
-    if rank == 0 and world == 1 and args.pmc:
-        del states
-        torch.cuda.empty_cache()  # the PMC child run allocates its own states
-        try:
-            traffic = merge_traffic(args) or traffic
-        except Exception as e:  # noqa: BLE001 -- reported, never fatal
-            traffic = {"bytes": None, "source": f"live PMC failed: {type(e).__name__}"}
-        res["roofline"]["traffic"] = traffic["bytes"]
-        res["roofline"]["traffic_source"] = traffic["source"]
+    if pre["traffic"] is not None:
+        res["roofline"]["traffic"] = pre["traffic"]["bytes"]
+        res["roofline"]["traffic_source"] = pre["traffic"]["source"]
     if rank == 0:
         print(json.dumps(res), flush=True)
     finish(world)
@@ -825,7 +832,7 @@ def merge_cpu_baseline(states, seconds):
 
 # ---- config 5: streaming ingest + unique crash/hang table --------------------------------------
 
-def main_stream(args):
+def main_stream(args, pre=None):
     """BASELINE config 5: config-2 traces in pageable host memory, produced into the pinned
     ingest ring (kbz_ring_acquire/submit: double-buffered hipMemcpyAsync, triage with XXH64)
     and the crash/hang traces' keys {XXH64, outcome class} inserted into the unique crash/hang
@@ -858,7 +865,8 @@ def main_stream(args):
         _, _, x64, o = item
         keys = torch.from_numpy(np.stack([x64.view(np.int64), o.astype(np.int64)], 1)).to(dev)
         mask = torch.from_numpy(o != 0).to(dev)
-        n_new = n_new + dedup_sharded(table, keys, mask, rank, world).sum()  # no host sync
+        # every rank's slot is `slot` rows: a fixed cap, no host sync
+        n_new = n_new + dedup_sharded(table, keys, mask, rank, world, cap=slot).sum()
 
     def step(i):
         r, o = ctx.ring_acquire()  # waits for this slot's previous batch: its results are in
@@ -960,7 +968,7 @@ def table_insert_rate(dev, n=1 << 20, batches=8):
 
 # ---- plugin per-exec latency -------------------------------------------------------------------
 
-def main_plugin(args):
+def main_plugin(args, pre=None):
     """Per-exec latency of the instrumentation plugin (libkbz_plugin.so, include/kbz_plugin.h)
     driven like fuzzer/main.c:370-418: every exec's raw trace is recorded, its novelty queried.
     Batch 1 = the unmodified per-exec loop (is_new_path after each exec flushes a batch of one);
@@ -1023,11 +1031,45 @@ def main_plugin(args):
     print(json.dumps(res), flush=True)
 
 
+def profile_first(args):
+    """The profiler children of a one-GPU run (rank 0), started before this process touches the
+    GPU: the kernel trace and the PMC passes of config 2 / 3, the PMC passes of the merge fold.
+    Failures are reported in the line, never fatal."""
+    pre = {"traffic": None, "ktrace": None, "valu": None}
+    if args.gpus != 1 or os.environ.get("WORLD_SIZE", "1") != "1":
+        return pre
+    if args.workload in ("config2", "config3"):
+        if args.ktrace:
+            try:
+                pre["ktrace"] = live_kernel_trace(args, steps=min(args.steps, 12))
+            except Exception as e:  # noqa: BLE001
+                pre["ktrace"] = {"avg_ms": None,
+                                 "what": f"kernel trace failed: {type(e).__name__}: {e}"[:300]}
+        if args.pmc:
+            try:
+                pre["traffic"] = live_traffic(args)
+            except Exception as e:  # noqa: BLE001
+                pre["traffic"] = {"bytes": None, "source": f"live PMC failed: {type(e).__name__}"}
+            if args.workload == "config3":
+                try:
+                    pre["valu"] = live_valu(args)
+                except Exception as e:  # noqa: BLE001
+                    pre["valu"] = {"instructions_per_launch": None,
+                                   "what": f"live PMC failed: {type(e).__name__}"}
+    elif args.workload == "merge" and args.pmc:
+        try:
+            pre["traffic"] = merge_traffic(args)
+        except Exception as e:  # noqa: BLE001
+            pre["traffic"] = {"bytes": None, "source": f"live PMC failed: {type(e).__name__}"}
+    return pre
+
+
 def main():
     args = parse()
     maybe_launch(args)
+    pre = profile_first(args)  # before any GPU call in this process
     {"merge": main_merge, "stream": main_stream, "plugin": main_plugin}.get(
-        args.workload, main_triage)(args)
+        args.workload, main_triage)(args, pre)
 
 
 if __name__ == "__main__":

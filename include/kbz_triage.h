@@ -247,8 +247,9 @@ int kbz_merge_and_fill_device(uint8_t *d_out, size_t n, size_t state_bytes, kbz_
  * GPUs (ncclCommInitAll + ncclAllGather, librccl loaded at run time) followed by a local AND on
  * every device, or peer / device-local copies of every partial to worker 0's device and one AND
  * there -- and the merged state is copied to host `out`.  exchange: KBZ_EXCHANGE_AUTO (RCCL when
- * the devices are distinct and more than one, else copies), KBZ_EXCHANGE_COPY, KBZ_EXCHANGE_RCCL
- * (fails if RCCL cannot be used).  A device may be listed several times (several workers on one
+ * the devices are distinct and more than one, else copies; copies also when any RCCL step fails:
+ * the partial folds are intact), KBZ_EXCHANGE_COPY, KBZ_EXCHANGE_RCCL (fails if RCCL cannot be
+ * used; one distinct device is a valid one-rank communicator).  A device may be listed several times (several workers on one
  * GPU: the copy path).  *used_out (or NULL) gets the exchange actually used.  Synchronous. */
 enum kbz_exchange { KBZ_EXCHANGE_AUTO = 0, KBZ_EXCHANGE_COPY = 1, KBZ_EXCHANGE_RCCL = 2 };
 int kbz_merge_and_fill_devices(uint8_t *out, size_t n, size_t state_bytes, kbz_merge_fill_fn fill,

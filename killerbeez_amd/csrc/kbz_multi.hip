@@ -112,6 +112,52 @@ struct DevScope {  // restore the calling thread's device
   }
 };
 
+// RCCL exchange: one ncclAllGather of every worker's fold over comms from ncclCommInitAll (one
+// rank per distinct GPU), then a local AND of the gathered rows on every device.  Every stream
+// is synchronised before the communicators are destroyed (no collective or AND still queued on
+// a comm being torn down).  Returns 0, or -1 with *why set; the partial folds are left intact,
+// so a caller may still exchange them by copies.
+int rccl_exchange(std::vector<Worker> &ws, const std::vector<int> &devs, size_t state_bytes,
+                  std::string *why) {
+  Rccl &r = rccl();
+  const size_t W = ws.size();
+  std::vector<ncclComm_t> comms(W, nullptr);
+  ncclResult_t e = r.init_all(comms.data(), (int)W, devs.data());
+  if (e != ncclSuccess) {
+    *why = std::string("ncclCommInitAll: ") + r.err_str(e);
+    return -1;
+  }
+  int rc = 0;
+  e = r.group_start();
+  for (size_t w = 0; w < W && e == ncclSuccess; w++) {
+    (void)hipSetDevice(ws[w].dev);
+    e = r.all_gather(ws[w].part, ws[w].gather, state_bytes, ncclUint8, comms[w], ws[w].s);
+  }
+  const ncclResult_t eg = r.group_end();
+  if (e == ncclSuccess) e = eg;
+  if (e != ncclSuccess) {
+    *why = std::string("ncclAllGather: ") + r.err_str(e);
+    rc = -1;
+  }
+  for (size_t w = 0; w < W && rc == 0; w++) {  // every device ANDs the gathered rows locally
+    if (hipSetDevice(ws[w].dev) != hipSuccess ||
+        kbz_merge_and_device(ws[w].merged, ws[w].gather, W, state_bytes, ws[w].s)) {
+      *why = std::string("local AND after the all-gather: ") + kbz_last_error();
+      rc = -1;
+    }
+  }
+  for (size_t w = 0; w < W; w++) {  // drain before the comms go away
+    (void)hipSetDevice(ws[w].dev);
+    if (hipStreamSynchronize(ws[w].s) != hipSuccess && rc == 0) {
+      *why = "stream synchronise after the all-gather failed";
+      rc = -1;
+    }
+  }
+  for (auto c : comms)
+    if (c) (void)r.destroy(c);
+  return rc;
+}
+
 }  // namespace
 
 extern "C" int kbz_merge_and_fill_devices(uint8_t *out, size_t n, size_t state_bytes,
@@ -192,33 +238,18 @@ extern "C" int kbz_merge_and_fill_devices(uint8_t *out, size_t n, size_t state_b
   for (size_t w = 0; w < W; w++)
     if (ws[w].rc) return fail_multi("worker " + std::to_string(w) + " (device " +
                                     std::to_string(ws[w].dev) + "): " + ws[w].err);
-  // 2. exchange the partial folds
+  // 2. exchange the partial folds.  AUTO falls back to copies when any RCCL step fails (the
+  //    folds are intact); an explicit RCCL request fails loudly instead.
+  bool copied = !use_rccl;
   if (use_rccl) {
-    Rccl &r = rccl();
-    std::vector<ncclComm_t> comms(W, nullptr);
-    ncclResult_t e = r.init_all(comms.data(), (int)W, devs.data());
-    if (e != ncclSuccess) return fail_multi(std::string("ncclCommInitAll: ") + r.err_str(e));
-    struct Comms {
-      Rccl &r;
-      std::vector<ncclComm_t> &c;
-      ~Comms() {
-        for (auto x : c)
-          if (x) (void)r.destroy(x);
-      }
-    } guard{r, comms};
-    e = r.group_start();
-    for (size_t w = 0; w < W && e == ncclSuccess; w++) {
-      (void)hipSetDevice(ws[w].dev);
-      e = r.all_gather(ws[w].part, ws[w].gather, state_bytes, ncclUint8, comms[w], ws[w].s);
+    std::string why;
+    if (rccl_exchange(ws, devs, state_bytes, &why)) {
+      if (exchange == KBZ_EXCHANGE_RCCL) return fail_multi(why);
+      copied = true;
+      if (used_out) *used_out = KBZ_EXCHANGE_COPY;
     }
-    const ncclResult_t eg = r.group_end();
-    if (e == ncclSuccess) e = eg;
-    if (e != ncclSuccess) return fail_multi(std::string("ncclAllGather: ") + r.err_str(e));
-    for (size_t w = 0; w < W; w++) {  // every device ANDs the gathered rows locally
-      MHIP(hipSetDevice(ws[w].dev));
-      if (kbz_merge_and_device(ws[w].merged, ws[w].gather, W, state_bytes, ws[w].s)) return -1;
-    }
-  } else {
+  }
+  if (copied) {
     Worker &k0 = ws[0];
     MHIP(hipSetDevice(k0.dev));
     for (size_t w = 0; w < W; w++) {

@@ -69,11 +69,14 @@ class _Clock:
 
 
 def triage_sharded(engine, traces, outcome, counts, rank, world, want=1, group=None,
-                   device=None, timings=None):
+                   device=None, timings=None, force_collective=False):
     """Run one rank's part of a sharded batch.  counts[r] = number of traces on rank r (host
     ints, known to every rank).  Returns the engine's output dict (hnb, h32, ...).
     timings: a list that receives this batch's phase times {pass1, link, reduce, collective,
-    finish} in ms (HIP events on a GPU, read with timing_summary after the steps)."""
+    finish} in ms (HIP events on a GPU, read with timing_summary after the steps).
+    force_collective: run the all-gathers even at world 1 (a one-rank RCCL communicator
+    exercises the exchange path on a one-GPU box)."""
+    coll = world > 1 or force_collective
     device = device if device is not None else traces.device
     clk = _Clock(device) if timings is not None else None
     mark = clk.mark if clk else (lambda name: None)
@@ -89,7 +92,7 @@ def triage_sharded(engine, traces, outcome, counts, rank, world, want=1, group=N
         engine.shard_last_row(buf[:m])
         engine.shard_last_hash(buf[m:m + 8].view(torch.int32))
         mark("link")
-        bufs = _all_gather(buf, world, group) if world > 1 else buf.view(1, -1)
+        bufs = _all_gather(buf, world, group) if coll else buf.view(1, -1)
         mark("collective")
         rows, pairs = bufs[:, :m], bufs[:, m:m + 8].view(torch.int32)
         prev = [r for r in nonempty if r < rank]
@@ -106,7 +109,7 @@ def triage_sharded(engine, traces, outcome, counts, rank, world, want=1, group=N
     agg = torch.empty(nb, dtype=torch.uint8, device=device)
     engine.shard_aggregate(agg)
     mark("reduce")
-    if world > 1:
+    if coll:
         allagg = _all_gather(agg, world, group)
         mark("collective")
         total = torch.empty(nb, dtype=torch.uint8, device=device)
@@ -136,7 +139,7 @@ def timing_summary(timings):
 
 # ---- merger across GPUs (BASELINE config 4) ----------------------------------
 
-def merge_sharded(states, world, group=None, fold=None, out=None):
+def merge_sharded(states, world, group=None, fold=None, out=None, force_collective=False):
     """The merger's AND-fold (merger/merger.c:79-99 -> afl_merge afl_instrumentation.c:123-140)
     over states spread across ranks: every rank folds its own states (rows of `states`, any
     count, possibly 0) with one local AND-fold, the ranks all-gather their partial folds
@@ -144,11 +147,11 @@ def merge_sharded(states, world, group=None, fold=None, out=None):
     and commutative, so the result equals the sequential fold of all states in any order.
     `fold(rows, out=None)` is the local AND-fold (default: kbz_merge_and_device); RCCL has no
     bitwise-AND reduction, hence all-gather + local fold.  Returns the merged state (every
-    rank holds it)."""
+    rank holds it).  force_collective: all-gather even at world 1."""
     if fold is None:
         from .triage import merge_and as fold
     local = fold(states)
-    if world == 1:
+    if world == 1 and not force_collective:
         if out is not None:
             out.copy_(local)
             return out
@@ -159,24 +162,29 @@ def merge_sharded(states, world, group=None, fold=None, out=None):
 
 # ---- unique crash/hang table across GPUs (BASELINE config 5) ----------------
 
-def dedup_sharded(table, keys, mask, rank, world, group=None, cap=None):
+def dedup_sharded(table, keys, mask, rank, world, group=None, cap=None, force_collective=False):
     """The reference's insert-if-absent set novelty (linux_ipt_instrumentation.c:412-424: new iff
     the key was absent; HASH_ADD keeps insertion order) over a batch sharded by contiguous trace
     index.  keys: this rank's [n_r, 2] int64 keys (e.g. {XXH64 of the transformed trace,
     outcome class}: triage.dedup_keys); mask: [n_r] bool/uint8, rows that take part (crash and
     hang traces).  Every rank's rows are all-gathered in rank order -- i.e. in global trace
     order -- as ONE fixed-shape buffer of cap rows per rank {key, mask} (padding rows masked
-    out; cap = the largest shard, default n_r: equal shards), and inserted as one ordered, masked
-    batch into every rank's replica `table` (any object with UniqueSet.insert(keys, mask)), so
-    all replicas stay identical and the first occurrence in global order is the new one.  No
-    host synchronisation and no host-side concatenation: the masking happens in the insert.
-    Returns this rank's is_new [n_r] uint8 (0 for masked-out rows)."""
+    out; cap = the largest shard), and inserted as one ordered, masked batch into every rank's
+    replica `table` (any object with UniqueSet.insert(keys, mask)), so all replicas stay
+    identical and the first occurrence in global order is the new one.  With `cap` given there
+    is no host synchronisation and no host-side concatenation (the masking happens in the
+    insert); without it, one all_reduce(MAX) of the shard sizes finds it (one host sync), so
+    unequal shards are always handled.  Returns this rank's is_new [n_r] uint8 (0 for masked-out
+    rows).  force_collective: all-gather even at world 1."""
     dev = keys.device
     n = keys.shape[0]
     m8 = mask.to(torch.int64).view(-1, 1)
-    if world == 1:
+    if world == 1 and not force_collective:
         return table.insert(keys, mask=mask.to(torch.uint8)).to(torch.uint8)
-    cap = n if cap is None else cap
+    if cap is None:
+        c = torch.tensor([n], dtype=torch.int64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.MAX, group=group)
+        cap = int(c.item())
     if n > cap:
         raise ValueError("dedup_sharded: shard larger than cap")
     buf = torch.zeros((cap, 3), dtype=torch.int64, device=dev)

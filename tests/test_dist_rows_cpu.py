@@ -74,11 +74,11 @@ def _worker(rank, world, port, counts, q):
     merged = merge_sharded(torch.from_numpy(s[lo:lo + n].copy()).view(n, SB), world, fold=_fold)
     tab = OrderedSetTable()
     news = []
-    for b in range(2):  # two batches: the replica carries over
-        k, m = _keys(sum(counts), 20 + b)
+    for b in range(3):  # three batches: the replica carries over; the last one without a cap
+        k, m = _keys(sum(counts), 20 + b)   # (the ranks negotiate it: unequal shards)
         news.append(dedup_sharded(tab, torch.from_numpy(k[lo:lo + n].copy()),
                                   torch.from_numpy(m[lo:lo + n].copy()), rank, world,
-                                  cap=max(counts)).numpy())
+                                  cap=max(counts) if b < 2 else None).numpy())
     q.put((rank, merged.numpy(), news, list(tab.keys)))
     dist.destroy_process_group()
 
@@ -115,7 +115,7 @@ def test_merge_and_dedup_sharded(oracle_lib, counts):
         exp &= s[i]
     # dedup: one insert-if-absent pass in global trace order
     seen, exp_new = {}, []
-    for b in range(2):
+    for b in range(3):
         k, m = _keys(n, 20 + b)
         e = np.zeros(n, np.uint8)
         for j in range(n):
@@ -127,6 +127,6 @@ def test_merge_and_dedup_sharded(oracle_lib, counts):
     for r in range(world):
         np.testing.assert_array_equal(res[r][0], exp)
         assert res[r][2] == list(seen)  # same keys, same insertion order, on every replica
-    for b in range(2):
+    for b in range(3):
         got = np.concatenate([res[r][1][b] for r in range(world)])
         np.testing.assert_array_equal(got, exp_new[b])

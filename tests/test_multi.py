@@ -1,8 +1,9 @@
 """The merger fold sharded over GPUs from C (kbz_merge_and_fill_devices, include/kbz_triage.h):
 merger/merger.c:79-104 with the states split across workers, one per GPU (several may share a
 GPU), exchanged by copies or RCCL and ANDed.  On a one-GPU box the workers share cuda:0 and the
-copy path runs; the RCCL all-gather path needs distinct GPUs and is unmeasured here (it runs on a
-multi-GPU node: its results are the same AND)."""
+copy path runs, and the RCCL path runs as a one-rank communicator (devices=[0]); the RCCL
+all-gather between distinct GPUs is exercised only where the box has two or more (unmeasured
+on the one-GPU box: its results are the same AND)."""
 import os
 
 import numpy as np
@@ -54,6 +55,48 @@ def test_merge_devices_errors(gpu):
         merge_and_devices(st, devices=[0, 0], exchange=EXCHANGE_RCCL)
     with pytest.raises(RuntimeError, match="out of range"):
         merge_and_devices(st, devices=[0, 999])
+
+
+def _rccl_mapped():
+    with open("/proc/self/maps") as f:
+        return any("librccl" in line for line in f)
+
+
+@pytest.mark.gpu
+def test_merge_devices_rccl_one_rank(gpu):
+    """The RCCL exchange itself (dlopen'd librccl, ncclCommInitAll, grouped ncclAllGather, local
+    AND, streams drained before the comms are destroyed) on one distinct device: the reference's
+    golden merge (afl_merge over tests/golden/merge.npz) and a random fold."""
+    from tests.test_golden import _merge_fixture
+
+    st, exp = _merge_fixture()
+    out, used = merge_and_devices(st.reshape(5, -1), devices=[0], exchange=EXCHANGE_RCCL)
+    assert used == EXCHANGE_RCCL
+    np.testing.assert_array_equal(out.reshape(3, -1), exp)
+    big = _states(3000, 3 * 65536, 21)
+    out, used = merge_and_devices(big, devices=[0], exchange=EXCHANGE_RCCL)
+    assert used == EXCHANGE_RCCL
+    np.testing.assert_array_equal(out, np.bitwise_and.reduce(big, axis=0))
+    assert _rccl_mapped(), "librccl was not loaded"
+
+
+@pytest.mark.gpu
+def test_merge_devices_distinct_gpus(gpu):
+    """Two or more distinct GPUs: AUTO takes RCCL (or falls back to copies if an RCCL step
+    fails), both exchanges forced; every result is the AND.  Skipped on a one-GPU box."""
+    import torch
+
+    nd = torch.cuda.device_count()
+    if nd < 2:
+        pytest.skip("needs two or more GPUs")
+    st = _states(4001, 3 * 8192, 33)
+    exp = np.bitwise_and.reduce(st, axis=0)
+    for ex in (None, EXCHANGE_COPY, EXCHANGE_RCCL):
+        kw = {} if ex is None else {"exchange": ex}
+        out, used = merge_and_devices(st, devices=list(range(nd)), **kw)
+        if ex is not None:
+            assert used == ex
+        np.testing.assert_array_equal(out, exp)
 
 
 @pytest.mark.gpu
