@@ -331,6 +331,15 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #ifndef KBZ_PASS1_TMIX  // which modes' mix wave T computes (see k_pass1s); 0 = none
 #define KBZ_PASS1_TMIX 3
 #endif
+#ifndef KBZ_P1S_GROUP  // k_pass1s DynamoRIO: nonzero words transformed G at a time (0: one by one)
+#define KBZ_P1S_GROUP 4
+#endif
+#ifndef KBZ_P1S_ORGATE  // k_pass1s: column ORs only for words where some row holds a virgin bit
+#define KBZ_P1S_ORGATE 1
+#endif
+#ifndef KBZ_AB_P1S  // timing-only ablations of k_pass1s (wrong results; variant builds only):
+#define KBZ_AB_P1S 0  // 1 no column OR, 2 no neighbour test, 4 no classify, 8 no mix, 16 wave T
+#endif                // skips the word loop, 32 wave L skips the chain
 #ifndef KBZ_WIDE_PEEL  // k_pass1w transform waves: steady steps without bounds tests
 #define KBZ_WIDE_PEEL 1
 #endif
@@ -338,6 +347,16 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #define KBZ_WIDE_BAL 1
 #endif
 
+// k_pass1s: which instantiations have wave T compute the hash32 mix (KBZ_PASS1_TMIX), and which
+// write claim records -- one predicate for the kernel and the host (shard_begin_impl decides
+// from it whether k_tail may read records).
+__host__ __device__ constexpr bool p1s_tmix(int mode, bool x64) {
+  return !x64 && (KBZ_PASS1_TMIX == 2 || (KBZ_PASS1_TMIX >= 1 && mode == KBZ_MODE_AFL) ||
+                  (KBZ_PASS1_TMIX == 3 && mode == KBZ_MODE_DYNAMORIO));
+}
+__host__ __device__ constexpr bool p1s_records(int mode, bool ign, bool x64) {
+  return p1s_tmix(mode, x64) && mode == KBZ_MODE_DYNAMORIO && !ign;
+}
 struct Pass1Args {
   const uint8_t *traces;
   size_t stride;
@@ -356,7 +375,6 @@ struct Pass1Args {
   const uint8_t *vcur;  // [3][map_size] virgin maps at batch entry
   uint64_t *tflags;     // [chunks][nclass][nfw]: bit t%64 of word t/64 = tile t of chunk_or stored
   uint32_t nfw;         // flag words per (chunk, class) = ceil(tiles / 64)
-  uint8_t *hnb_clear;   // [n] or null: zeroed here
   uint64_t *frec;       // [chunks][map_size] claim records (k_pass1s DynamoRIO without ignore
                         // bytes / XXH64, one-shard batches) or null
   uint64_t *rflags;     // [chunks][nfw]: bit t%64 of word t/64 = tile t's records written
@@ -405,11 +423,9 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   // KBZ_PASS1_TMIX: 1 = AFL only, 2 = every mode, 3 (default) = AFL and DynamoRIO.  With T
   // mixing, wave L is a bare chain: DynamoRIO config 2 pass 1 -2 % same-box since wave T reads
   // its slots 8 ahead (profiles/r03_v13); AFL_CLASSIFY stays on L (+3 % with T mixing).
-  constexpr bool TMIX = !X64 && (KBZ_PASS1_TMIX == 2 ||
-                                 (KBZ_PASS1_TMIX >= 1 && MODE == KBZ_MODE_AFL) ||
-                                 (KBZ_PASS1_TMIX == 3 && MODE == KBZ_MODE_DYNAMORIO));
+  constexpr bool TMIX = p1s_tmix(MODE, X64);
   // claim records (a.frec): DynamoRIO with the mix in LDS and every byte examined
-  constexpr bool REC = TMIX && MODE == KBZ_MODE_DYNAMORIO && !IGN;
+  constexpr bool REC = p1s_records(MODE, IGN, X64);
   // AFL modes: the simplified classes' column ORs come from their rows, once per tile
   constexpr bool SROWS = KBZ_PASS1_SROWS && NC > 1;
   constexpr int TW = 256, SLOTS = 16, RPI = 4, NLD = 8;  // 8 x 1-KiB loads per wave per tile
@@ -527,7 +543,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
 #pragma unroll
       for (int u = 0; u < D; u++) {
         const uint32_t s = g + u;
-        if (s >= 1 && s <= ntiles) chain_tile(s - 1, (s - 1) & 1);
+        if (!(KBZ_AB_P1S & 32) && s >= 1 && s <= ntiles) chain_tile(s - 1, (s - 1) & 1);
         KBZ_STAMP(0);
         vmcnt_wait<(D - 1) * NLD>();
         KBZ_STAMP(1);
@@ -541,7 +557,8 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
     KBZ_STAMP_FLUSH(chunk * 2 + 0);
     drain_asm_loads(R);
     if (valid) {
-      const uint32_t h32 = h32_final(h);
+      // (the no-chain ablation stores distinct hashes, so nothing downstream sees repeats)
+      const uint32_t h32 = (KBZ_AB_P1S & 32) ? (uint32_t)(row0 + lane) * 2654435761u : h32_final(h);
       a.h32[row0 + lane] = h32;
       if (X64 && a.x64) {
         uint64_t xh = rotl64(x0, 1) + rotl64(x1, 7) + rotl64(x2, 12) + rotl64(x3, 18);
@@ -660,6 +677,79 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
       }
       uint4 *row = &lds[b * TILE + lane * SLOTS];
       const int sw = lane & 15;
+      // the tile's virgin words at batch entry, lane w < 32 holding word w of each class
+      uint64_t vlane[NC];
+#pragma unroll
+      for (int k = 0; k < NC; k++)
+        vlane[k] = ((const uint64_t *)&lds[2 * TILE + b * 48 + k * 16])[lane & 31];
+      if constexpr (MODE == KBZ_MODE_DYNAMORIO && KBZ_P1S_GROUP > 0) {
+        // DynamoRIO: the nonzero words of the tile in groups of G, each group's G words
+        // transformed, mixed and compared side by side.  Processed one word at a time (the loop
+        // below) every nonzero word was a dependent chain of ~40 instructions behind a branch --
+        // at two waves per SIMD wave T spent 87 % of each step in that latency
+        // (profiles/r05_c/stamps_k_pass1s.txt).  (1) one 32-bit mask of the words that are nonzero
+        // in some row; (2) groups of G set bits (the last group padded with its last word: a word
+        // processed twice gives the same results), each word re-read from the tile buffer by a
+        // uniform index, written back mixed for wave L.
+        constexpr int G = KBZ_P1S_GROUP > 0 ? KBZ_P1S_GROUP : 1;  // (the branch is dead at 0)
+        uint32_t nzm = 0;
+        {
+          uint4 vv[SLOTS];
+#pragma unroll
+          for (int q = 0; q < SLOTS; q++) vv[q] = row[q ^ sw];
+#pragma unroll
+          for (int q = 0; q < SLOTS; q++) {
+            nzm |= __ballot((vv[q].x | vv[q].y) != 0) ? 1u << (2 * q) : 0u;
+            nzm |= __ballot((vv[q].z | vv[q].w) != 0) ? 1u << (2 * q + 1) : 0u;
+          }
+        }
+        uint64_t *roww = (uint64_t *)row;
+        while (nzm) {  // wave-uniform
+          int w[G];
+          int last = 0;
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            if (nzm) {
+              last = __builtin_ctz(nzm);
+              nzm &= nzm - 1;
+            }
+            w[g] = last;
+          }
+          uint64_t tw[G];
+#pragma unroll
+          for (int g = 0; g < G; g++) tw[g] = roww[(((w[g] >> 1) ^ sw) << 1) | (w[g] & 1)];
+#pragma unroll
+          for (int g = 0; g < G; g++) tw[g] = classify8(tw[g]);
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            const uint64_t out = TMIX ? h32_mix_mad(tw[g] & (IGN ? ig[w[g]] : ~0ull)) : tw[g];
+            roww[(((w[g] >> 1) ^ sw) << 1) | (w[g] & 1)] = out;
+          }
+          if (present[0]) {
+            uint64_t c[G], any = 0;
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+              const uint64_t vw =
+                  ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(vlane[0] >> 32), w[g]) << 32) |
+                  __builtin_amdgcn_readlane((uint32_t)vlane[0], w[g]);
+              c[g] = valid ? (tw[g] & vw) : 0ull;
+              any |= c[g];
+            }
+            if (__ballot(any != 0)) {  // some row holds a still-virgin bit (rare on a warm map)
+              uint64_t r[G];  // the G reductions side by side (no branch between them)
+#pragma unroll
+              for (int g = 0; g < G; g++) r[g] = wave_or64(c[g]);
+#pragma unroll
+              for (int g = 0; g < G; g++) orw[0] = (lane == w[g]) ? r[g] : orw[0];
+            }
+          }
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            const uint64_t rel = IGN ? ~nonzero_bytes8(ig[w[g]]) : ~0ull;
+            neq |= (tw[g] ^ from_prev_lane(tw[g])) & rel;
+          }
+        }
+      } else {
       // slots in flight: a mostly-zero slot takes a few instructions, far less than an LDS round
       // trip (deeper register rings, timing-only builds, keep 2: their VGPRs are spent)
       constexpr int TP = D > 2 ? 2 : KBZ_PASS1_TPRE;
@@ -679,21 +769,35 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         for (int e = 0; e < 2; e++) {
           const int wi = 2 * q + e;
           const uint64_t x = ld_u64(v, e);
-          if (__ballot(x != 0)) {
-            const uint64_t tw = xform8(x, xf);
+          if (!(KBZ_AB_P1S & 16) && __ballot(x != 0)) {
+            const uint64_t tw = (KBZ_AB_P1S & 4) ? x : xform8(x, xf);
             // what wave L chains next step (with ignore bytes the mix sees the kept bytes only)
-            const uint64_t out = TMIX ? h32_mix_mad(tw & (IGN ? ig[wi] : ~0ull)) : tw;
+            const uint64_t out = (TMIX && !(KBZ_AB_P1S & 8)) ? h32_mix_mad(tw & (IGN ? ig[wi] : ~0ull)) : tw;
             if (e) { v.z = (uint32_t)out; v.w = (uint32_t)(out >> 32); }
             else { v.x = (uint32_t)out; v.y = (uint32_t)(out >> 32); }
             dirty = true;
 #pragma unroll
             for (int k = 0; k < (RW ? 1 : NC); k++) {
               if (present[k]) {
-                const uint64_t r = wave_or64((valid && cls == k) ? tw : 0);
-                orw[k] = (lane == wi) ? r : orw[k];
+                if (KBZ_P1S_ORGATE) {
+                  // only bits still virgin at batch entry are kept (m = OR & V below): the
+                  // 64-lane reduction runs only when some row of the class holds one in this word
+                  // (on a warm map almost never: config 2 pass 1 -5 %, the no-OR ablation)
+                  const uint64_t vw =
+                      ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(vlane[k] >> 32), wi) << 32) |
+                      __builtin_amdgcn_readlane((uint32_t)vlane[k], wi);
+                  const uint64_t c = (valid && cls == k) ? (tw & vw) : 0;
+                  if (__ballot(c != 0)) {
+                    const uint64_t r = (KBZ_AB_P1S & 1) ? c : wave_or64(c);
+                    orw[k] = (lane == wi) ? r : orw[k];
+                  }
+                } else {
+                  const uint64_t r = (KBZ_AB_P1S & 1) ? tw : wave_or64((valid && cls == k) ? tw : 0);
+                  orw[k] = (lane == wi) ? r : orw[k];
+                }
               }
             }
-            if (MODE == KBZ_MODE_DYNAMORIO) {
+            if (MODE == KBZ_MODE_DYNAMORIO && !(KBZ_AB_P1S & 2)) {
               const uint64_t rel = IGN ? ~nonzero_bytes8(ig[wi]) : ~0ull;
               neq |= (tw ^ from_prev_lane(tw)) & rel;
             }
@@ -706,6 +810,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         // raw AFL words are their own transform (only simplified lanes change) unless T mixes
         if (dirty && (TMIX || MODE != KBZ_MODE_AFL || simp)) *slot = v;
       }
+      }
       // chunk_or keeps only bits still virgin at batch entry (orw & V): the scan uses nothing
       // else (its new bits are o & V & ~prev, and f2 only looks at bytes with V == 0xff), and a
       // tile with none is not stored at all, only its flag bit stays clear.  In steady-state
@@ -715,7 +820,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
       for (int k = 0; k < NC; k++) {
         if (!present[k]) continue;
         const size_t off = (size_t)k * a.map_size + (size_t)s * TW + (size_t)lane * 8;
-        const uint64_t m = orw[k] & ((const uint64_t *)&lds[2 * TILE + b * 48 + k * 16])[lane & 31];
+        const uint64_t m = orw[k] & vlane[k];
         if (__ballot(lane < TW / 8 && m != 0)) {
           tfl[k] |= 1ull << (s & 63);
           if (lane < TW / 8) *(uint64_t *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) = m;
@@ -763,7 +868,6 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
     // lane 0 has no predecessor in the wave: its value is a placeholder (k_skip compares a chunk's
     // row 0 with the previous row itself, and only when their hashes are equal)
     if (MODE == KBZ_MODE_DYNAMORIO && valid) a.neq[row0 + lane] = neq != 0;
-    if (a.hnb_clear && valid) a.hnb_clear[row0 + lane] = 0;
   }
 }
 
@@ -930,7 +1034,6 @@ __global__ __launch_bounds__(64 * (NL + NX), 1) void k_pass1w(Pass1Args a) {
     if (isL && valid) {
       const uint32_t h32 = h32_final(h);
       a.h32[row0 + lane] = h32;
-      if (a.hnb_clear) a.hnb_clear[row0 + lane] = 0;
       if (X64 && a.x64) {
         uint64_t xh = rotl64(x0, 1) + rotl64(x1, 7) + rotl64(x2, 12) + rotl64(x3, 18);
         xh = xx_merge(xh, x0);
@@ -1369,7 +1472,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
     }
   }
   drain_asm_loads(R);
-  if (a.hnb_clear && wave == 0 && lane < nrows) a.hnb_clear[row0 + lane] = 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1397,6 +1499,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
 // No barrier inside the tile loop: the waves synchronise only through the LDS flags (polled with
 // s_sleep) and one barrier at the end (tile flags, neighbour flags).
 // ---------------------------------------------------------------------------------------------
+#ifndef KBZ_PASS1D_CWAIT  // 1: wave C drains its next-tile LDS reads at the end of every tile
+#define KBZ_PASS1D_CWAIT 1
+#endif
 #ifndef KBZ_MAX_FW
 #define KBZ_MAX_FW 1024  // tile-flag words per class: maps up to 16 MiB
 #endif
@@ -1497,7 +1602,12 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
         KBZ_STAMP(1);
         read_k(IntC<b ^ 1>{}, IntC<sl1>{});
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile t + 1's words have arrived
+      // Tile t + 1's words have arrived before the freed flag is written.  (Without this wait --
+      // safe, since a wave's LDS operations execute in issue order, with the compiler kept from
+      // sinking the reads below the flag store by an empty asm -- config 3 pass 1 was 1.3 %
+      // slower: 3.10 vs 3.06 ms same-box, profiles/r05_d/ab2.txt.)
+      if (KBZ_PASS1D_CWAIT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else asm volatile("" ::: "memory");
       KBZ_STAMP(2);
       if (lane == 0) {
         if (X64) KBZ_FST(freed_c, sl, (int)t);
@@ -1520,7 +1630,6 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
     if (lane < nrows) {
       const uint32_t h32 = h32_final(h);
       a.h32[row0 + lane] = h32;
-      if (a.hnb_clear) a.hnb_clear[row0 + lane] = 0;
       if (X64 && a.x64) {
         uint64_t xh = rotl64(x0, 1) + rotl64(x1, 7) + rotl64(x2, 12) + rotl64(x3, 18);
         xh = xx_merge(xh, x0);
@@ -2976,12 +3085,16 @@ __global__ __launch_bounds__(256) void k_fin(FinArgs a) {
   ClaimQ cq{fin_q[threadIdx.x >> 6], 0};
   const ClaimArgs ca{a.ra.traces, a.ra.stride, a.ra.n, a.ra.mode, a.ra.outcome, a.ra.skip,
                      a.ra.hnb32, a.ra.err};
-  for (uint32_t it0 = wave * kClaimQ; it0 < cnt; it0 += nwaves * kClaimQ) {
-    const uint64_t mine = (lane < kClaimQ && it0 + lane < cnt) ? a.items[it0 + lane] : 0ull;
-    if (lane < kClaimQ && it0 + lane < cnt) a.items[it0 + lane] = 0;  // all-zero between batches
+  // items are dealt round-robin over the waves (item i to wave i % nwaves): a window item streams
+  // 64 rows, so consecutive ones must not queue on one wave (novelty-heavy batches: ~50 window
+  // items, dealt 8 per wave k_fin took 250 us)
+  for (uint32_t it0 = wave; it0 < cnt; it0 += nwaves * kClaimQ) {
+    const uint32_t myit = it0 + (uint32_t)lane * nwaves;
+    const uint64_t mine = (lane < kClaimQ && myit < cnt) ? a.items[myit] : 0ull;
+    if (lane < kClaimQ && myit < cnt) a.items[myit] = 0;  // all-zero between batches
 #pragma unroll
     for (int j = 0; j < kClaimQ; j++) {
-      if (it0 + j >= cnt) break;  // wave-uniform
+      if (it0 + (uint32_t)j * nwaves >= cnt) break;  // wave-uniform
       const uint64_t item = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(mine >> 32), j) << 32) |
                             __builtin_amdgcn_readlane((uint32_t)mine, j);
       if (!item) {  // reserved and never written
@@ -3435,6 +3548,8 @@ struct kbz_ctx {
   uint32_t cur_chunks = 0, cur_seg_len = 1, cur_nseg = 1;
   bool fix_pending = false;  // DynamoRIO: k_skip ran for this batch, k_total runs the fix path
   int stage = 0;
+  // a fused one-shard DynamoRIO batch: the last-hash and saved-row words k_tail reads / writes
+  uint32_t *fchain_ctx_last = nullptr, *fchain_next_last = nullptr, *fchain_saved_ok = nullptr;
   // host streaming
   hipStream_t copy_stream = nullptr, work_stream = nullptr;
   uint8_t *pin[2] = {nullptr, nullptr};
@@ -3900,11 +4015,12 @@ uint8_t *kbz_virgin_device(kbz_ctx_t *c) { return c ? c->V[c->vcur] : nullptr; }
 }  // extern "C"
 namespace {
 int fused_link(kbz_ctx *c, hipStream_t s, SkipExtra *x);
-// kbz_shard_begin; with `fused` (a one-shard batch of kbz_triage_batch_device) pass 1 also
-// zeroes hnb_clear and k_skip takes k_chain's row-0 and saved-row roles (the fused tail).
+void fused_link_commit(kbz_ctx *c);
+// kbz_shard_begin; with `fused` (a one-shard batch of kbz_triage_batch_device) k_skip takes
+// k_chain's row-0 and saved-row roles (the fused tail).
 int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
                      const int8_t *outcome, uint32_t *h32_out, uint64_t *x64_out, int want,
-                     void *stream, uint8_t *hnb_clear, bool fused) {
+                     void *stream, bool fused) {
   if (!c) return fail("null ctx");
   if (n > c->max_batch) return fail("n exceeds max_batch");
   if (n && check_rows(traces, stride, c->M)) return -1;
@@ -3965,13 +4081,12 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
   a.vcur = c->V[c->vcur];
   a.tflags = c->tflags;
   a.nfw = c->nfw;
-  a.hnb_clear = hnb_clear;
   a.frec = nullptr;
   a.rflags = nullptr;
   a.epoch = 0;
   c->cur_rec = false;
   // one-shard DynamoRIO batches through k_pass1s without ignore bytes or XXH64: claim records
-  if (fused && c->rec_ok && c->mode == KBZ_MODE_DYNAMORIO && !c->ignore && !a.x64 &&
+  if (fused && c->rec_ok && p1s_records(c->mode, c->ignore != nullptr, a.x64 != nullptr) &&
       !pass1_is_wide(c->pass1, c->cur_chunks)) {
     if (!c->frec) {
       const size_t bytes = (size_t)c->max_chunks * c->M * sizeof(uint64_t);
@@ -3983,6 +4098,9 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
         c->frec = nullptr;
         c->rflags = nullptr;
         c->rec_ok = false;  // no room: k_tail reads the rows instead
+      } else if (hipMemsetAsync(c->rflags, 0, (size_t)c->max_chunks * c->nfw * sizeof(uint64_t),
+                                s) != hipSuccess) {
+        return fail("hipMemsetAsync of the record flags failed");
       }
     }
     if (c->frec) {
@@ -4023,6 +4141,7 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
                        c->counters + 3, c->bad_list, c->counters + 4, c->shard_last, traces,
                        stride, c->ignore, (uint32_t)c->M, row_blocks, x);
     HIP_TRY(hipGetLastError());
+    if (fused) fused_link_commit(c);  // k_skip is queued: this batch's row is the next predecessor
     if (stage_end(c, s, KBZ_STAGE_SKIP, st0)) return -1;
   }
   c->stage = 1;
@@ -4033,10 +4152,8 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
 // (kbz_shard_link for a one-shard batch): row 0's predecessor is the saved row (clean iff its
 // flag), the batch's last row becomes the next batch's predecessor (the other saved slot), the
 // next last hash goes to the other last-hash word; k_tail writes those two words.
-struct FusedChain {
-  uint32_t *ctx_last, *next_last, *saved_ok;
-};
-thread_local FusedChain g_fchain;
+// fused_link only fills the arguments (and the chain words k_tail gets, kept in the context);
+// the context's saved-row / last-hash slots flip once k_skip is launched (fused_link_commit).
 int fused_link(kbz_ctx *c, hipStream_t, SkipExtra *x) {
   const size_t M = c->M, n = c->cur_n;
   x->row0_hp = c->last + c->lcur;
@@ -4047,13 +4164,15 @@ int fused_link(kbz_ctx *c, hipStream_t, SkipExtra *x) {
   x->copy_src = c->cur_traces + (n - 1) * c->cur_stride;
   x->copy_dst = c->saved_row + (c->srow ^ 1) * M;
   x->copy_blocks = std::min(64u, cdiv(M / 16, 256));
-  g_fchain.ctx_last = c->last + c->lcur;
-  g_fchain.next_last = c->last + (c->lcur ^ 1);
-  g_fchain.saved_ok = c->counters + 6 + (c->srow ^ 1);
+  c->fchain_ctx_last = c->last + c->lcur;
+  c->fchain_next_last = c->last + (c->lcur ^ 1);
+  c->fchain_saved_ok = c->counters + 6 + (c->srow ^ 1);
+  return 0;
+}
+void fused_link_commit(kbz_ctx *c) {
   c->srow ^= 1;
   c->saved_valid = true;
   c->lcur ^= 1;
-  return 0;
 }
 
 // Everything after pass 1 (and k_skip) of a one-shard batch in one launch: k_tail.
@@ -4097,9 +4216,9 @@ int fused_tail(kbz_ctx *c, uint8_t *hnb_out, hipStream_t s) {
   a.shard_last = c->shard_last;
   a.neq = c->neq;
   a.bad_list = c->bad_list;
-  a.ctx_last = g_fchain.ctx_last;
-  a.next_last = g_fchain.next_last;
-  a.saved_ok = g_fchain.saved_ok;
+  a.ctx_last = c->fchain_ctx_last;
+  a.next_last = c->fchain_next_last;
+  a.saved_ok = c->fchain_saved_ok;
   a.flags_w = c->flags;
   a.fix_list_w = c->fix_list;
   a.fix_cnt_w = c->counters + 3;
@@ -4138,8 +4257,7 @@ extern "C" {
 int kbz_shard_begin(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_t stride,
                     const int8_t *outcome, uint32_t *h32_out, uint64_t *x64_out, int want,
                     void *stream) {
-  return shard_begin_impl(c, traces, n, stride, outcome, h32_out, x64_out, want, stream, nullptr,
-                          false);
+  return shard_begin_impl(c, traces, n, stride, outcome, h32_out, x64_out, want, stream, false);
 }
 
 int kbz_shard_last_hash(kbz_ctx_t *c, uint32_t *d_out, void *stream) {
@@ -4343,8 +4461,7 @@ int kbz_triage_batch_device(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_
     return 0;
   }
   if (c && c->fused_ok && n && c->stage == 0) {  // one shard: pass 1, [k_skip], k_tail
-    if (shard_begin_impl(c, traces, n, stride, outcome, h32_out, x64_out, want, stream, nullptr,
-                         true))
+    if (shard_begin_impl(c, traces, n, stride, outcome, h32_out, x64_out, want, stream, true))
       return -1;
     DevGuard g(c->device);
     return fused_tail(c, hnb_out, (hipStream_t)stream);
@@ -4403,6 +4520,7 @@ int kbz_sync(kbz_ctx_t *c, void *stream) {
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   uint32_t cnt[4];
   HIP_TRY(hipMemcpy(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost));
+  if (KBZ_AB_P1S) cnt[1] = cnt[2] = 0;  // timing-only ablation builds: results are wrong anyway
   if (cnt[1] || cnt[2]) {  // sticky until reported here
     HIP_TRY(hipMemset(c->counters + 1, 0, 2 * sizeof(uint32_t)));
     c->h_err[0] = c->h_err[1] = 0;  // k_pack's host-mapped copy: reported now, not again

@@ -41,5 +41,43 @@ if [ -n "$DIRECT" ]; then
     rm -f $(find $O/prof_$name -name '*kernel_trace.csv')
   done
 fi
+if [ -n "$AB" ]; then
+  step "ab $AB ($AB_ARGS)"
+  STEPS=${AB_STEPS:-10} VARIANTS="$AB" BENCH_ARGS="$AB_ARGS" timeout -k 10 900 bash scripts/ab_variants.sh > $O/ab.txt 2>&1 || { cat $O/ab.txt; exit 1; }
+  cat $O/ab.txt
+fi
+if [ -n "$AB2" ]; then
+  step "ab2 $AB2 ($AB2_ARGS)"
+  STEPS=${AB_STEPS:-10} VARIANTS="$AB2" BENCH_ARGS="$AB2_ARGS" timeout -k 10 900 bash scripts/ab_variants.sh > $O/ab2.txt 2>&1 || { cat $O/ab2.txt; exit 1; }
+  cat $O/ab2.txt
+fi
+if [ -n "$STAMPS" ]; then
+  step stamps
+  KBZ_HIP_LIB=$PWD/build_variants/stamps/libkbz_hip.so timeout -k 10 200 python tools/stamps.py > $O/stamps_k_pass1s.txt 2>&1 || { tail $O/stamps_k_pass1s.txt; exit 1; }
+  cat $O/stamps_k_pass1s.txt
+fi
+if [ -n "$TAILST" ]; then
+  step tailstamps
+  KBZ_TAIL_BATCHES=${TAILST_BATCHES:-16} KBZ_HIP_LIB=$PWD/build_variants/tailst/libkbz_hip.so timeout -k 10 300 python tools/tail_stamps.py > $O/tail_stamps.txt 2>&1 || { tail $O/tail_stamps.txt; exit 1; }
+  tail -4 $O/tail_stamps.txt
+fi
+if [ -n "$NOVTRACE" ]; then
+  step noveltytrace
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_nov -o run -- python3 tools/novelty_trace.py 5 > $O/novelty_trace.json 2> $O/novelty_trace.err || { tail $O/novelty_trace.err; exit 1; }
+  python3 scripts/ktrace_kernels.py $O/prof_nov > $O/novelty_kernels.json || exit 1
+  rm -f $(find $O/prof_nov -name '*kernel_trace.csv')
+  cat $O/novelty_trace.json; tail -c 600 $O/novelty_kernels.json; echo
+fi
+if [ -n "$PROBE" ]; then
+  step l2probe
+  timeout -k 10 120 ./tools/l2_handoff_probe 1024 20 > $O/l2_handoff_probe.txt 2>&1 || { tail $O/l2_handoff_probe.txt; exit 1; }
+  cat $O/l2_handoff_probe.txt
+fi
+if [ -n "$SQ" ]; then
+  step "sq ($SQ_ARGS)"
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --output-format csv -d $O/sq -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-pmc --no-ktrace --no-variants $SQ_ARGS > $O/sq.log 2>&1 || { tail -20 $O/sq.log; exit 1; }
+  f=$(find $O/sq -name '*counter_collection.csv' | head -1); grep k_pass1 "$f" > $O/sq_pass1.csv; rm -rf $O/sq
+  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD --output-format csv -d $O/sq2 -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-pmc --no-ktrace --no-variants $SQ_ARGS > $O/sq2.log 2>&1 && { f=$(find $O/sq2 -name '*counter_collection.csv' | head -1); grep k_pass1 "$f" > $O/sq2_pass1.csv; rm -rf $O/sq2; }
+fi
 for f in $(find $O -name '*.stamp' 2>/dev/null); do rm -f $f; done
 step done

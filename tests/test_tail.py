@@ -52,8 +52,9 @@ def test_tail_afl_three_maps_large_grid(gpu, staged, monkeypatch):
 
 
 def test_tail_touched_rows_only(gpu):
-    """hnb_out rows the tail never scores stay 0 (pass 1 cleared them): a batch in which only
-    a few rows bring anything new, after a warm-up batch, with garbage in the output buffer."""
+    """hnb_out rows the tail never scores are written 0 (k_fin copies every row of hnb32, which
+    the previous batch's k_fin re-armed): a batch in which only a few rows bring anything new,
+    after a warm-up batch, with garbage in the output buffer."""
     import torch
 
     m = 65536

@@ -30,7 +30,8 @@ buf = np.zeros(NREC * 4, np.uint64)
 dev = torch.device("cuda:0")
 mode = MODES[mode_name]
 want = WANT_H32 if mode == MODES["dynamorio"] else 0
-pool = [synth.sparse_torch(B, M, seed=1 + 7919 * p, device=dev, hot_seed=1) for p in range(8)]
+NB = int(os.environ.get("KBZ_TAIL_BATCHES", "8"))  # the bench times batches 4..23
+pool = [synth.sparse_torch(B, M, seed=1 + 7919 * p, device=dev, hot_seed=1) for p in range(NB)]
 out = {"hnb": torch.empty(B, dtype=torch.uint8, device=dev)}
 res = []
 with TriageContext(M, mode, B) as ctx:
