@@ -331,6 +331,9 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #ifndef KBZ_PASS1_TMIX  // which modes' mix wave T computes (see k_pass1s); 0 = none
 #define KBZ_PASS1_TMIX 3
 #endif
+#ifndef KBZ_P1S_LEARLY  // k_pass1s wave L: issue each step's loads before its chain (ring D + 1)
+#define KBZ_P1S_LEARLY 1
+#endif
 #ifndef KBZ_P1S_GROUP  // k_pass1s DynamoRIO: nonzero words transformed G at a time (0: one by one)
 #define KBZ_P1S_GROUP 4
 #endif
@@ -339,7 +342,8 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #endif
 #ifndef KBZ_AB_P1S  // timing-only ablations of k_pass1s (wrong results; variant builds only):
 #define KBZ_AB_P1S 0  // 1 no column OR, 2 no neighbour test, 4 no classify, 8 no mix, 16 wave T
-#endif                // skips the word loop, 32 wave L skips the chain
+#endif                // skips the word loop, 32 wave L skips the chain, 64 no segment-OR
+                      // atomics, 128 no chunk_or stores
 #ifndef KBZ_WIDE_PEEL  // k_pass1w transform waves: steady steps without bounds tests
 #define KBZ_WIDE_PEEL 1
 #endif
@@ -472,10 +476,18 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
       lds[b * TILE + rr * SLOTS + (ls ^ (rr & 15))] = make_uint4(v.x, v.y, v.z, v.w);
     }
   };
+  // L's register ring is one slot deeper than T's: each step issues its next loads BEFORE the
+  // chain and stores the oldest slot after it, so the chain no longer delays L's loads (the
+  // chain-free ablation was 4 % faster, profiles/r05/ab_p1s_ablations_d2.txt).  Both waves run
+  // the same number of steps (barriers): 0..ntiles rounded up to a multiple of both rings, so
+  // neither unrolled loop needs a guard around its asm loads.
+  constexpr int DL = KBZ_P1S_LEARLY ? D + 1 : D;
+  constexpr int SP = DL == D ? D : D * DL;
+  const uint32_t nsteps = (ntiles + SP) / SP * SP;
   if (wave == 0) {
-    u32x4 R[D][NLD];
+    u32x4 R[DL][NLD];
 #pragma unroll
-    for (int d = 0; d < D; d++) load_half(R[d], d);
+    for (int d = 0; d < DL; d++) load_half(R[d], d);
     // ------------------------------------------------------------------ wave L
     uint64_t h = (uint64_t)(kHashConst ^ a.map_size);
     uint64_t x0 = kXP1 + kXP2, x1 = kXP2, x2 = 0, x3 = 0 - kXP1;
@@ -532,26 +544,46 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
       }
     };
     // prologue: own half of tile 0 -> buffer 0 (T transforms it at step 0)
-    vmcnt_wait<(D - 1) * NLD>();
+    vmcnt_wait<(DL - 1) * NLD>();
     store_half(R[0], 0);
-    load_half(R[0], D);
+    if (DL == D) load_half(R[0], D);
     lds_barrier();  // (A)
     KBZ_STAMP_DECL;
-    // step s: chain tile s-1, store own half of tile s+1 (ring slot (s+1)%D) into the buffer
-    // just chained, prefetch tile s+1+D into that slot.
-    for (uint32_t g = 0; g <= ntiles; g += D) {
+    if (DL > D) {
+      // step s: prefetch tile s+DL into ring slot (s+DL)%DL (its tile s was stored last step),
+      // chain tile s-1, store own half of tile s+1 (slot (s+1)%DL) into the buffer just chained
+      for (uint32_t g = 0; g < nsteps; g += DL) {
 #pragma unroll
-      for (int u = 0; u < D; u++) {
-        const uint32_t s = g + u;
-        if (!(KBZ_AB_P1S & 32) && s >= 1 && s <= ntiles) chain_tile(s - 1, (s - 1) & 1);
-        KBZ_STAMP(0);
-        vmcnt_wait<(D - 1) * NLD>();
-        KBZ_STAMP(1);
-        store_half(R[(u + 1) % D], (s + 1) & 1);
-        load_half(R[(u + 1) % D], s + 1 + D);
-        KBZ_STAMP(2);
-        lds_barrier();
-        KBZ_STAMP(3);
+        for (int u = 0; u < DL; u++) {
+          const uint32_t s = g + u;
+          load_half(R[u], s + DL);
+          if (!(KBZ_AB_P1S & 32) && s >= 1 && s <= ntiles) chain_tile(s - 1, (s - 1) & 1);
+          KBZ_STAMP(0);
+          vmcnt_wait<(DL - 1) * NLD>();
+          KBZ_STAMP(1);
+          store_half(R[(u + 1) % DL], (s + 1) & 1);
+          KBZ_STAMP(2);
+          lds_barrier();
+          KBZ_STAMP(3);
+        }
+      }
+    } else {
+      // step s: chain tile s-1, store own half of tile s+1 (ring slot (s+1)%D) into the buffer
+      // just chained, prefetch tile s+1+D into that slot.
+      for (uint32_t g = 0; g < nsteps; g += D) {
+#pragma unroll
+        for (int u = 0; u < D; u++) {
+          const uint32_t s = g + u;
+          if (!(KBZ_AB_P1S & 32) && s >= 1 && s <= ntiles) chain_tile(s - 1, (s - 1) & 1);
+          KBZ_STAMP(0);
+          vmcnt_wait<(D - 1) * NLD>();
+          KBZ_STAMP(1);
+          store_half(R[(u + 1) % D], (s + 1) & 1);
+          load_half(R[(u + 1) % D], s + 1 + D);
+          KBZ_STAMP(2);
+          lds_barrier();
+          KBZ_STAMP(3);
+        }
       }
     }
     KBZ_STAMP_FLUSH(chunk * 2 + 0);
@@ -693,7 +725,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         // uniform index, written back mixed for wave L.
         constexpr int G = KBZ_P1S_GROUP > 0 ? KBZ_P1S_GROUP : 1;  // (the branch is dead at 0)
         uint32_t nzm = 0;
-        {
+        if (!(KBZ_AB_P1S & 16)) {
           uint4 vv[SLOTS];
 #pragma unroll
           for (int q = 0; q < SLOTS; q++) vv[q] = row[q ^ sw];
@@ -823,12 +855,13 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         const uint64_t m = orw[k] & vlane[k];
         if (__ballot(lane < TW / 8 && m != 0)) {
           tfl[k] |= 1ull << (s & 63);
-          if (lane < TW / 8) *(uint64_t *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) = m;
+          if (!(KBZ_AB_P1S & 128) && lane < TW / 8)
+            *(uint64_t *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) = m;
           if (REC && a.frec && tile_records(s, b, m)) rfl |= 1ull << (s & 63);
         }
         // segment aggregate, restricted to still-virgin bits like chunk_or (its consumers only
         // use it under & V: k_scan's segment test and V' = V & ~total): almost never an atomic
-        if (lane < TW / 8 && m)
+        if (!(KBZ_AB_P1S & 64) && lane < TW / 8 && m)
           atomicOr((unsigned long long *)(a.segor + (size_t)seg * NC * a.map_size + off),
                    (unsigned long long)m);
         if ((s & 63) == 63 || s + 1 == ntiles) {
@@ -845,7 +878,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
     KBZ_STAMP_DECL;
     // step s: store own half of tile s (ring slot s%D), prefetch tile s+D into that slot,
     // transform tile s.  T issues NLD + NC loads per step.
-    for (uint32_t g = 0; g <= ntiles; g += D) {
+    for (uint32_t g = 0; g < nsteps; g += D) {
 #pragma unroll
       for (int u = 0; u < D; u++) {
         const uint32_t s = g + u;
@@ -2461,7 +2494,10 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
 // chunk that belong to class k (and are not skipped) are walked in order with their running OR
 // `acc`: row r claims t_r & V & ~(prev | acc) (has_new_bits, afl_instrumentation.c:600-662, over
 // the window), and scores 2 if it is the first row with a nonzero byte where V is 0xff and prev
-// is 0 (:644-651).  Rows are loaded 8 at a time (1 KiB per row, coalesced).
+// is 0 (:644-651).  Rows are loaded KBZ_WIN_ROWS at a time (1 KiB per row, coalesced).
+#ifndef KBZ_WIN_ROWS  // rows of a window item in flight per round trip (8: novelty-heavy k_fin
+#define KBZ_WIN_ROWS 16  // spent 8 round trips per item)
+#endif
 struct ResolveArgs {  // what resolving a claim item needs (k_resolve, the fused tail)
   const uint8_t *traces;
   size_t stride;
@@ -2507,17 +2543,18 @@ __device__ __forceinline__ void resolve_window(const ResolveArgs &r, uint32_t ch
   const int xf = class_xf(r.mode, k);
   bool claimed = false;
   while (rows) {
-    int rr[8];
-    uint4 v[8];
+    constexpr int WR = KBZ_WIN_ROWS;
+    int rr[WR];
+    uint4 v[WR];
 #pragma unroll
-    for (int u = 0; u < 8; u++) {  // up to 8 rows' loads in flight
+    for (int u = 0; u < WR; u++) {  // up to WR rows' loads in flight
       rr[u] = rows ? __builtin_ctzll(rows) : -1;
       rows &= rows - 1;
       const uint64_t rw = row0 + (rr[u] >= 0 ? rr[u] : 0);
       v[u] = *(const uint4 *)(r.traces + rw * r.stride + cl);
     }
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
+    for (int u = 0; u < WR; u++) {
       if (rr[u] < 0) break;  // wave-uniform
       const uint64_t t0 = xform8((uint64_t)v[u].x | ((uint64_t)v[u].y << 32), xf) & rel0;
       const uint64_t t1 = xform8((uint64_t)v[u].z | ((uint64_t)v[u].w << 32), xf) & rel1;
@@ -2665,6 +2702,7 @@ struct TailArgs {
   uint32_t nfw;
   const uint32_t *listed;  // DynamoRIO: fix-list flags
   uint32_t win_items;
+  uint32_t inline_max;  // claimed bytes a wave resolves inline (KBZ_TAIL_INLINE_MAX)
   uint32_t *tail;
   uint32_t *shard_last;
   const uint64_t *frec;    // pass 1's claim records (null: none this batch)
@@ -2678,6 +2716,11 @@ struct TailArgs {
   uint32_t *saved_ok;
   uint32_t *flags_w, *fix_list_w, *fix_cnt_w;  // the walks' fix list (DynamoRIO)
 };
+#ifndef KBZ_TAIL_INLINE_MAX  // claimed bytes one k_tail wave resolves inline; the rest become
+#define KBZ_TAIL_INLINE_MAX 16  // items, dealt over all of k_fin's waves.  Fresh batches on a warm
+#endif                          // map stay inline (their busiest waves had 8-9); on all-0xff maps
+                                // the busiest waves had 40-50 and set k_tail's span
+                                // (profiles/r05/tail_stamps_novelty.txt)
 #ifndef KBZ_TAIL_INLINE  // 1: k_tail resolves claims of < win_items bytes itself, as k_scan does;
 #define KBZ_TAIL_INLINE 1  // 0: every claim is an item, resolved by k_fin over the whole grid
 #endif                     // (config 2 tail 64 -> 115 us: the 64-row byte reads are the cost)
@@ -2855,6 +2898,7 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
     ItemStage stg{stage_buf[threadIdx.x >> 6], 0u};
     __shared__ uint4 claim_q[4][kClaimQ];
     ClaimQ cq{claim_q[threadIdx.x >> 6], 0};
+    uint32_t inl = 0;  // claimed bytes this wave resolved inline (wave-uniform)
     const uint32_t seg_new = (send.x & vr.x & ~prev.x) | (send.y & vr.y & ~prev.y) |
                              (send.z & vr.z & ~prev.z) | (send.w & vr.w & ~prev.w);
     KBZ_TAIL_MARK();
@@ -2934,8 +2978,9 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
               const uint32_t ncl = wave_claimed_bytes(nb);  // the rest: read the rows
               if (!__ballot(nb.x | nb.y | nb.z | nb.w)) {
                 // every claimed byte had a record
-              } else if (KBZ_TAIL_INLINE && ncl < a.win_items) {
+              } else if (KBZ_TAIL_INLINE && ncl < a.win_items && inl + ncl <= a.inline_max) {
                 KBZ_TAIL_ADD(claims, ncl);
+                inl += ncl;
                 claims_enqueue(a.ca, k, cq, c, col, nb, vir, prev);
               } else {
                 KBZ_TAIL_ADD(win, 1);
@@ -3533,6 +3578,7 @@ struct kbz_ctx {
   uint64_t *items = nullptr;
   uint32_t item_cap = 0;
   uint32_t win_items = KBZ_WIN_ITEMS;  // claimed bytes per chunk x 1-KiB window: window item
+  uint32_t inline_max = KBZ_TAIL_INLINE_MAX;  // k_tail: inline claims per wave (tests: env)
   bool small_ok = true;  // k_small for small AFL batches (tests: KBZ_DEBUG_NO_SMALL=1 disables)
   uint32_t *counters = nullptr;  // [0] items, [1] overflow, [2] resolve error, [3] fix list,
                                  // [4] bad rows, [6..7] clean flags of the saved rows,
@@ -3874,6 +3920,7 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   if (const char *cap = getenv("KBZ_DEBUG_ITEM_CAP")) c->item_cap = std::max(1, atoi(cap));
   // tests only: force window items everywhere (1) or never (a large value)
   if (const char *w = getenv("KBZ_DEBUG_WIN_ITEMS")) c->win_items = (uint32_t)std::max(1, atoi(w));
+  if (const char *w = getenv("KBZ_DEBUG_TAIL_INLINE_MAX")) c->inline_max = (uint32_t)std::max(0, atoi(w));
   // tests only: small AFL batches through the general pipeline instead of k_small
   if (const char *w = getenv("KBZ_DEBUG_NO_SMALL")) c->small_ok = atoi(w) == 0;
   // tests only: one-shard batches through the staged kernels (k_chain ... k_pack) instead of k_tail
@@ -4209,6 +4256,7 @@ int fused_tail(kbz_ctx *c, uint8_t *hnb_out, hipStream_t s) {
   a.nfw = c->nfw;
   a.listed = dr ? c->flags : nullptr;
   a.win_items = c->win_items;
+  a.inline_max = c->inline_max;
   a.tail = c->tail;
   a.frec = c->cur_rec ? c->frec : nullptr;
   a.rflags = c->rflags;

@@ -58,7 +58,7 @@ if [ -n "$STAMPS" ]; then
 fi
 if [ -n "$TAILST" ]; then
   step tailstamps
-  KBZ_TAIL_BATCHES=${TAILST_BATCHES:-16} KBZ_HIP_LIB=$PWD/build_variants/tailst/libkbz_hip.so timeout -k 10 300 python tools/tail_stamps.py > $O/tail_stamps.txt 2>&1 || { tail $O/tail_stamps.txt; exit 1; }
+  KBZ_TAIL_NOVELTY=${TAILST_NOVELTY:-0} KBZ_TAIL_BATCHES=${TAILST_BATCHES:-16} KBZ_HIP_LIB=$PWD/build_variants/tailst/libkbz_hip.so timeout -k 10 300 python tools/tail_stamps.py > $O/tail_stamps.txt 2>&1 || { tail $O/tail_stamps.txt; exit 1; }
   tail -4 $O/tail_stamps.txt
 fi
 if [ -n "$NOVTRACE" ]; then

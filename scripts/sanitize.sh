@@ -19,6 +19,6 @@ PRE="$(gcc -print-file-name=libasan.so) $(gcc -print-file-name=libubsan.so)"
 export ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:abort_on_error=1:alloc_dealloc_mismatch=0:detect_odr_violation=0
 export UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1
 KBZ_PLUGIN_LIB=$PWD/$OUT/libkbz_plugin.so KBZ_ORACLE_LIB=$PWD/$OUT/libkbz_oracle.so \
-  LD_PRELOAD="$PRE" python -m pytest -q -p no:cacheprovider -m "not gpu" \
+  LD_PRELOAD="$PRE${LD_PRELOAD:+ $LD_PRELOAD}" python -m pytest -q -p no:cacheprovider -m "not gpu" \
   tests/test_plugin.py tests/test_plugin_fuzz.py tests/test_golden.py tests/test_oracle_pin.py "$@"
 echo "sanitizer suite clean"

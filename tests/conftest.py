@@ -31,3 +31,17 @@ def gpu():
 
     L.lib()  # fails loudly if the HIP library is missing
     return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="session")
+def product_isa(tmp_path_factory):
+    """Device ISA of the product kbz_triage.hip (gfx950), compiled once per session (CPU)."""
+    import subprocess
+
+    from killerbeez_amd import build
+
+    out = tmp_path_factory.mktemp("isa") / "kbz_triage.s"
+    subprocess.check_call([build.hipcc(), f"--offload-arch={build.ARCH}", "-O3", "-std=c++17",
+                           "--cuda-device-only", "-S", "-I", build.INC, "-I", build.CSRC,
+                           build.HIP_SOURCES[0], "-o", str(out)], stderr=subprocess.DEVNULL)
+    return out.read_text()

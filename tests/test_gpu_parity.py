@@ -750,9 +750,10 @@ def test_claim_overflow_is_reported_once(gpu, monkeypatch):
         assert p.result(tk) == exp["hnb"][j]
 
 
+@pytest.mark.parametrize("inl", [None, "0", "1000000"], ids=["inline16", "inline0", "inline-all"])
 @pytest.mark.parametrize("win", ["1", "16", "1000000"], ids=["all-windows", "default", "no-windows"])
 @pytest.mark.parametrize("mode", MODES)
-def test_claims_window_and_byte_items(gpu, mode, win, monkeypatch):
+def test_claims_window_and_byte_items(gpu, mode, win, inl, monkeypatch):
     """The claim paths give identical results: k_scan resolving a window's few claimed bytes
     itself (one byte of each of the chunk's rows per claim, 8 claims per round trip; the
     per-byte items of KBZ_SCAN_INLINE=0 builds follow the same rule in k_resolve) and window
@@ -761,6 +762,8 @@ def test_claims_window_and_byte_items(gpu, mode, win, monkeypatch):
     past the end; partial last chunk; DynamoRIO with ignore bytes and repeated execs (skipped
     rows must not claim), AFL with hangs/crashes (simplified classes: every byte claims)."""
     monkeypatch.setenv("KBZ_DEBUG_WIN_ITEMS", win)
+    if inl is not None:  # the fused tail's inline-claim budget per wave (the rest: byte items)
+        monkeypatch.setenv("KBZ_DEBUG_TAIL_INLINE_MAX", inl)
     rng = np.random.default_rng(int(win) % 97 + mode)
     for m, n in [(65536, 700), (19 * 256, 200), (1 << 20, 70)]:
         t = synth.uniform_np(n, m, seed=m + n, density=0.3)

@@ -1,0 +1,168 @@
+// tools/patprobe2.hip -- calibration probe (not part of the product): what does pass 1's LDS
+// staging cost on top of its access pattern?  One chunk = 64 rows of a [n x M] row-major batch
+// (stride S), streamed in tiles of TW bytes of every row by W = 2 waves (32 rows each), as
+// k_pass1s does.  Modes:
+//   0  register loads only (tools/patprobe.hip's pattern): D tiles in flight per wave;
+//   1  register loads -> XOR-swizzled ds_write_b128 -> raw barrier -> every wave reads the whole
+//      tile row-per-lane (SLOTS ds_read_b128, as waves L and T do) -- k_pass1s's structure
+//      without its compute, 2 LDS buffers, D register tiles in flight;
+//   2  LDS-DMA (global_load_lds_dwordx4, swizzle on the source address) into an NB-buffer ring,
+//      counted vmcnt, raw barrier, the same row-per-lane reads; NB - 1 tiles in flight.
+// Build: hipcc --offload-arch=gfx950 -O3 tools/patprobe2.hip -o tools/patprobe2
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int N>
+__device__ __forceinline__ void vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+// LDS-DMA as inline asm (the builtin makes hipcc wait vmcnt(0) before every LDS read, draining
+// the ring): M0 = the wave-uniform LDS byte address, written and restored in the same statement
+__device__ __forceinline__ void glds16(const unsigned char *g, unsigned lds_byte) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(lds_byte) : "memory");
+}
+__device__ __forceinline__ void asm_ld16(u32x4 &r, const unsigned char *p) {
+  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r) : "v"(p) : "memory");
+}
+
+template <int MODE, int TW, int D, int NB>
+__global__ __launch_bounds__(128) void probe(const unsigned char *base, size_t M, size_t S,
+                                             unsigned *out, const unsigned char *vmap) {
+  constexpr int SLOTS = TW / 16, RPI = 64 / SLOTS, NLD = 32 / RPI;  // loads per wave per tile
+  constexpr int TILE = 64 * SLOTS;                                   // uint4 per tile buffer
+  constexpr int NBUF = MODE == 2 ? NB : (MODE >= 1 ? 2 : 1);
+  __shared__ uint4 lds[NBUF * TILE + 64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lr = lane / SLOTS, ls = lane % SLOTS;
+  const unsigned char *cb = base + (size_t)blockIdx.x * 64 * S;
+  const int ntiles = (int)(M / TW);
+  u32x4 acc = {0, 0, 0, 0};
+  auto consume = [&](int b) {  // row-per-lane reads of buffer b
+    const uint4 *row = &lds[b * TILE + lane * SLOTS];
+    const int sw = lane & (SLOTS - 1);
+#pragma unroll
+    for (int q = 0; q < SLOTS; q++) {
+      const uint4 v = row[q ^ sw];
+      acc |= u32x4{v.x, v.y, v.z, v.w};
+    }
+  };
+  if constexpr (MODE == 0 || MODE == 1 || MODE == 3) {
+    // MODE 3: wave 1 also loads the tile's 16-B virgin words (a cached 64 KiB map, like wave T)
+    constexpr int NV = MODE == 3 ? 1 : 0;
+    u32x4 r[D][NLD + NV];
+    auto load = [&](u32x4 (&rr)[NLD + NV], int t) {
+      const int tt = t < ntiles ? t : ntiles - 1;
+#pragma unroll
+      for (int i = 0; i < NLD; i++) {
+        const int row = 32 * wave + RPI * i + lr;
+        asm_ld16(rr[i], cb + (size_t)row * S + (size_t)tt * TW + ls * 16);
+      }
+      if (NV) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rr[NLD]) : "v"(vmap + (size_t)tt * TW + (lane & (SLOTS - 1)) * 16) : "memory");
+    };
+#pragma unroll
+    for (int d = 0; d < D; d++) load(r[d], d);
+    for (int t0 = 0; t0 < ntiles; t0 += D) {
+#pragma unroll
+      for (int d = 0; d < D; d++) {
+        const int t = t0 + d;
+        vmwait<(D - 1) * (NLD + NV)>();
+        if (MODE == 0) {
+#pragma unroll
+          for (int i = 0; i < NLD; i++) acc |= r[d][i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < NLD; i++) {
+            const int rr = 32 * wave + RPI * i + lr;
+            const u32x4 v = r[d][i];
+            lds[(t & 1) * TILE + rr * SLOTS + (ls ^ (rr & (SLOTS - 1)))] = make_uint4(v.x, v.y, v.z, v.w);
+          }
+          if (NV && wave == 1 && lane < SLOTS) {
+            const u32x4 v = r[d][NLD];
+            lds[NBUF * TILE + lane] = make_uint4(v.x, v.y, v.z, v.w);
+          }
+        }
+        load(r[d], t + D);
+        if (MODE >= 1) {
+          raw_barrier();
+          consume(t & 1);
+        }
+      }
+    }
+    vmwait<0>();
+#pragma unroll
+    for (int d = 0; d < D; d++)
+#pragma unroll
+      for (int i = 0; i < NLD + NV; i++) asm volatile("" ::"v"(r[d][i]));
+  } else {
+    // LDS-DMA: instruction i of this wave fills rows 32 wave + RPI i .. + RPI - 1 of the buffer
+    // (1 KiB, lane-linear); lane l fetches the global slot that lands at its linear position
+    auto dma = [&](int t) {
+      const int tt = t < ntiles ? t : ntiles - 1;
+      const int b = t % NB;
+#pragma unroll
+      for (int i = 0; i < NLD; i++) {
+        const int rr = 32 * wave + RPI * i + lr;
+        const int q = ls ^ (rr & (SLOTS - 1));
+        glds16(cb + (size_t)rr * S + (size_t)tt * TW + q * 16,
+               __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)&lds[b * TILE + (32 * wave + RPI * i) * SLOTS]));
+      }
+    };
+#pragma unroll
+    for (int t = 0; t < NB - 1; t++) dma(t);
+    for (int t = 0; t < ntiles; t++) {
+      vmwait<(NB - 2) * NLD>();
+      raw_barrier();
+      dma(t + NB - 1);
+      consume(t % NB);
+    }
+    vmwait<0>();
+  }
+  if ((acc.x | acc.y | acc.z | acc.w) == 0xdeadbeefu) out[0] = 1;
+}
+
+template <int MODE, int TW, int D, int NB>
+void run(const unsigned char *p, size_t n, size_t M, size_t S, unsigned *o) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  float best = 1e9, sum = 0;
+  for (int r = 0; r < 6; r++) {
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL((probe<MODE, TW, D, NB>), dim3(n / 64), dim3(128), 0, 0, p, M, S, o, p);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms;
+    (void)hipEventElapsedTime(&ms, a, b);
+    if (r) {
+      best = ms < best ? ms : best;
+      sum += ms;
+    }
+  }
+  printf("mode %d TW %4d D %d NB %d: best %.4f ms avg %.4f ms  %.1f GB/s (best)\n", MODE, TW, D,
+         NB, best, sum / 5, n * M / (best * 1e-3) / 1e9);
+}
+
+int main() {
+  const size_t n = 65536, M = 65536, S = 65536;
+  unsigned char *p;
+  unsigned *o;
+  if (hipMalloc(&p, n * S) != hipSuccess || hipMalloc(&o, 4) != hipSuccess) return 1;
+  (void)hipMemset(p, 1, n * S);
+  (void)hipDeviceSynchronize();
+  // register modes only at D = 2: deeper rings here lack k_pass1s's register-safe waits
+  // (tools/vmem_hazard_cfg.py flags them) and one faulted on the GPU (profiles/r05/patprobe2.txt)
+  run<0, 256, 2, 0>(p, n, M, S, o);
+  run<1, 256, 2, 0>(p, n, M, S, o);
+  run<3, 256, 2, 0>(p, n, M, S, o);
+  run<2, 256, 0, 4>(p, n, M, S, o);
+  run<2, 128, 0, 4>(p, n, M, S, o);
+  return 0;
+}

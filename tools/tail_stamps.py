@@ -34,8 +34,13 @@ NB = int(os.environ.get("KBZ_TAIL_BATCHES", "8"))  # the bench times batches 4..
 pool = [synth.sparse_torch(B, M, seed=1 + 7919 * p, device=dev, hot_seed=1) for p in range(NB)]
 out = {"hnb": torch.empty(B, dtype=torch.uint8, device=dev)}
 res = []
+NOVELTY = os.environ.get("KBZ_TAIL_NOVELTY") == "1"  # every batch on all-0xff maps
 with TriageContext(M, mode, B) as ctx:
     for i, (t, oc) in enumerate(pool):
+        if NOVELTY and i:
+            ctx.set_virgin(np.full((3, M), 0xFF, np.uint8))
+            ctx.last_hash = 0
+            torch.cuda.synchronize()
         f(buf.ctypes.data, 0)  # clears the records
         ctx.triage(t, oc, want, out=out)
         torch.cuda.synchronize()
