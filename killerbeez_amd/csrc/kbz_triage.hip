@@ -1532,6 +1532,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
 // No barrier inside the tile loop: the waves synchronise only through the LDS flags (polled with
 // s_sleep) and one barrier at the end (tile flags, neighbour flags).
 // ---------------------------------------------------------------------------------------------
+#ifndef KBZ_PASS1D_READ2  // k_pass1d wave C: the next tile's 16 reads in the first half of the chain
+#define KBZ_PASS1D_READ2 0
+#endif
 #ifndef KBZ_PASS1D_CWAIT  // 1: wave C drains its next-tile LDS reads at the end of every tile
 #define KBZ_PASS1D_CWAIT 1
 #endif
@@ -1594,7 +1597,14 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
       constexpr int b = decltype(bc)::value, sl = decltype(sc)::value, sl1 = (sl + 1) % RING;
 #pragma unroll
       for (int q = 0; q < SLOTS; q++) {
-        kb[b ^ 1][q] = kring[sl1 * TILE + lane * SLOTS + (q ^ sw)];
+        if (KBZ_PASS1D_READ2) {  // two reads per chain step in the first half: all 16 are in
+          if (q < SLOTS / 2) {   // flight by mid-tile, none left for the end-of-tile wait
+            kb[b ^ 1][2 * q] = kring[sl1 * TILE + lane * SLOTS + ((2 * q) ^ sw)];
+            kb[b ^ 1][2 * q + 1] = kring[sl1 * TILE + lane * SLOTS + ((2 * q + 1) ^ sw)];
+          }
+        } else {
+          kb[b ^ 1][q] = kring[sl1 * TILE + lane * SLOTS + (q ^ sw)];
+        }
         __builtin_amdgcn_sched_barrier(0);
         const uint4 kq = kb[b][q];
         h = h32_step_fast(h, (uint64_t)kq.x | ((uint64_t)kq.y << 32));
