@@ -12,6 +12,7 @@
 //       0: sc1 loads, 1: plain loads, 2: sc0 sc1 loads (system scope), 3: nt loads
 //     and counts words that are not the producer's value.
 // Output per consumer: stale words, its XCD, K1's writer XCD, the producer's XCD, spin timeout.
+// With a third argument S, K2 also runs S load blocks beside the hand-offs (see stream_block).
 // Build: hipcc --offload-arch=gfx950 -O3 tools/l2_handoff_probe.hip -o tools/l2_handoff_probe
 #include <hip/hip_runtime.h>
 
@@ -46,9 +47,29 @@ __device__ __forceinline__ uint64_t ld(const uint64_t *p) {
   if (KIND == 3) return __builtin_nontemporal_load(p);
   return *(volatile const uint64_t *)p;
 }
+// Load: blocks 2R.. of K2 stream kStreamBytes each of another buffer (16-B nt loads, 8 in flight
+// per lane) and atomicMax a hash of what they read into a 64 Ki-entry score array -- what every
+// k_tail workgroup does beside a hand-off (the failing in-launch helpers ran under that load).
+constexpr size_t kStreamBytes = 4u << 20;
+__device__ __forceinline__ void stream_block(const uint4 *src, uint32_t *score) {
+  const int lane = threadIdx.x & 63;
+  uint32_t acc = 0;
+  for (size_t i = 0; i < kStreamBytes / 16; i += 64 * 8) {
+    uint4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[u] = src[i + u * 64 + lane];
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    atomicMax(&score[(acc * 2654435761u) >> 16], acc);
+  }
+}
 template <int KIND>
 __global__ void k2(uint64_t *d, uint32_t *flag, uint32_t R, uint64_t val, int warm,
-                   uint32_t *out, uint32_t ps, uint32_t cs) {
+                   uint32_t *out, uint32_t ps, uint32_t cs, const uint4 *sbuf, uint32_t *score) {
+  if (blockIdx.x >= 2 * R) {  // load blocks (dispatched after every producer and consumer)
+    stream_block(sbuf + (size_t)(blockIdx.x - 2 * R) * (kStreamBytes / 16), score);
+    return;
+  }
   // producer block p serves region (p + ps) % R, consumer block R + j region (j + cs) % R:
   // shifting the regions moves each role to other XCDs (blocks b and b + 8 share one)
   const uint32_t b = blockIdx.x < R ? (blockIdx.x + ps) % R : R + (blockIdx.x - R + cs) % R;
@@ -95,8 +116,15 @@ __global__ void k2(uint64_t *d, uint32_t *flag, uint32_t R, uint64_t val, int wa
 int main(int argc, char **argv) {
   const uint32_t R = argc > 1 ? atoi(argv[1]) : 1024;  // regions (producer / consumer pairs)
   const int reps = argc > 2 ? atoi(argv[2]) : 64;  // every (producer, consumer) shift pair
+  const uint32_t S = argc > 3 ? atoi(argv[3]) : 0;  // load blocks (each streams 4 MiB)
   uint64_t *d;
-  uint32_t *flag, *wx, *out;
+  uint32_t *flag, *wx, *out, *score;
+  uint4 *sbuf = nullptr;
+  CHECK(hipMalloc(&score, 65536 * 4));
+  if (S) {
+    CHECK(hipMalloc(&sbuf, (size_t)S * kStreamBytes));
+    CHECK(hipMemset(sbuf, 1, (size_t)S * kStreamBytes));
+  }
   CHECK(hipMalloc(&d, (size_t)R * kWords * 8));
   CHECK(hipMalloc(&flag, R * 4));
   CHECK(hipMalloc(&wx, R * 4));
@@ -111,10 +139,10 @@ int main(int argc, char **argv) {
         hipLaunchKernelGGL(k1, dim3(R), dim3(64), 0, 0, d, wx);
         CHECK(hipMemset(flag, 0, R * 4));
         const uint64_t val = 2 + r;
-        if (kind == 0) hipLaunchKernelGGL(k2<0>, dim3(2 * R), dim3(64), 0, 0, d, flag, R, val, warm, out, r % 8, (r / 8) % 8);
-        if (kind == 1) hipLaunchKernelGGL(k2<1>, dim3(2 * R), dim3(64), 0, 0, d, flag, R, val, warm, out, r % 8, (r / 8) % 8);
-        if (kind == 2) hipLaunchKernelGGL(k2<2>, dim3(2 * R), dim3(64), 0, 0, d, flag, R, val, warm, out, r % 8, (r / 8) % 8);
-        if (kind == 3) hipLaunchKernelGGL(k2<3>, dim3(2 * R), dim3(64), 0, 0, d, flag, R, val, warm, out, r % 8, (r / 8) % 8);
+        if (kind == 0) hipLaunchKernelGGL(k2<0>, dim3(2 * R + S), dim3(64), 0, 0, d, flag, R, val, warm, out, r % 8, (r / 8) % 8, sbuf, score);
+        if (kind == 1) hipLaunchKernelGGL(k2<1>, dim3(2 * R + S), dim3(64), 0, 0, d, flag, R, val, warm, out, r % 8, (r / 8) % 8, sbuf, score);
+        if (kind == 2) hipLaunchKernelGGL(k2<2>, dim3(2 * R + S), dim3(64), 0, 0, d, flag, R, val, warm, out, r % 8, (r / 8) % 8, sbuf, score);
+        if (kind == 3) hipLaunchKernelGGL(k2<3>, dim3(2 * R + S), dim3(64), 0, 0, d, flag, R, val, warm, out, r % 8, (r / 8) % 8, sbuf, score);
         CHECK(hipDeviceSynchronize());
         CHECK(hipMemcpy(h.data(), out, R * 16, hipMemcpyDeviceToHost));
         CHECK(hipMemcpy(hw.data(), wx, R * 4, hipMemcpyDeviceToHost));
@@ -127,10 +155,10 @@ int main(int argc, char **argv) {
         }
       }
       static const char *names[4] = {"sc1", "plain", "sc0sc1", "nt"};
-      printf("load=%-6s warm=%d  stale blocks %llu / %llu  timeouts %llu | stale words by "
+      printf("S=%u load=%-6s warm=%d  stale blocks %llu / %llu  timeouts %llu | stale words by "
              "(consumer on K1-writer XCD, consumer on producer XCD): "
              "(n,n) %llu/%llu (n,y) %llu/%llu (y,n) %llu/%llu (y,y) %llu/%llu\n",
-             names[kind], warm, blocks_stale, (unsigned long long)R * reps, timeouts,
+             S, names[kind], warm, blocks_stale, (unsigned long long)R * reps, timeouts,
              st[0][0], cnt[0][0] * kWords, st[0][1], cnt[0][1] * kWords, st[1][0],
              cnt[1][0] * kWords, st[1][1], cnt[1][1] * kWords);
     }
