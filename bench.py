@@ -397,6 +397,10 @@ def live_kernel_trace(args, warmup=3, steps=12):
 
 # A/B only: KBZ_BENCH_P1_TIMING=0 times the steps without the pass-1 events (roofline invalid)
 P1_TIMING = os.environ.get("KBZ_BENCH_P1_TIMING", "1") != "0"
+# A/B only: KBZ_BENCH_P1_EVERY=k times one pass-1 launch in k (events on a dispatch leave ~5 us
+# of idle GPU behind it in a kernel trace, profiles/r05_evgap; sampling 1 in 4 did not change
+# ms_per_step beyond the ±2 % between processes, profiles/r05_every): default every launch
+P1_EVERY = max(1, int(os.environ.get("KBZ_BENCH_P1_EVERY", "1")))
 VALU_ISSUE_CYCLES = 4  # one wave64 integer VALU instruction per SIMD per 4 cycles (tools/xprobe,
                        # SQ_ACTIVE_INST_VALU = SQ_INSTS_VALU quad-cycles: profiles/r03_v8)
 SIMDS = 256 * 4
@@ -564,6 +568,7 @@ def main_triage(args, pre):
     if want:
         out["h32"] = torch.empty(B, dtype=torch.int32, device=dev)
     counts = [B] * world
+    timed_launches = []  # pass-1 launches timed by each timed() call
     phase_log = None  # list: per-batch phase timings of the sharded protocol (world > 1)
 
     def step(t, oc):
@@ -578,6 +583,7 @@ def main_triage(args, pre):
         events per stage) stays off here: it adds ~50 us per step; the warmup steps time stages."""
         barrier_sync(world, dev)
         ctx.sync()
+        ctx.time_pass1_every(P1_EVERY)
         ctx.time_pass1(P1_TIMING)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         t0 = time.perf_counter()
@@ -588,7 +594,9 @@ def main_triage(args, pre):
         barrier_sync(world, dev)
         el = time.perf_counter() - t0
         ms, launches = ctx.time_pass1(False)
+        ctx.time_pass1_every(1)
         ctx.sync()
+        timed_launches.append(launches)
         r = (max_over_ranks(el, world, dev), ms / launches if launches else float("nan"))
         return r + (ev[0].elapsed_time(ev[1]),) if events else r
 
@@ -603,6 +611,7 @@ def main_triage(args, pre):
     fresh = pool[args.warmup:] if npool > args.warmup else pool
     phase_log = [] if world > 1 else None
     elapsed, pass1_ms = timed(fresh, args.steps)
+    pass1_timed = timed_launches[-1]
     phases = timing_summary(phase_log) if phase_log else {}
     phase_log = None
     n_fresh = min(args.steps, len(fresh))
@@ -680,6 +689,9 @@ def main_triage(args, pre):
                      "traffic": traffic["bytes"], "traffic_source": traffic["source"],
                      "kernel": kname,
                      "avg_launch_ms": round(pass1_ms, 4),
+                     "timed_launches": pass1_timed,
+                     "timed_launches_note": f"HIP events on one pass-1 launch in {P1_EVERY} of "
+                                            "the timed steps",
                      "algorithmic_bytes_per_launch": B * M},
         "pass1_share_of_step": round(pass1_ms / ms_per_step, 4),
         "variants": variants,

@@ -115,6 +115,10 @@ int kbz_ctx_stats(kbz_ctx_t *ctx, uint32_t *out);
  * the previous call (waiting for them), then enables (enable != 0) or disables timing of later
  * launches.  Diagnostics only (bench.py's roofline). */
 int kbz_ctx_time_pass1(kbz_ctx_t *ctx, int enable, double *total_ms, uint32_t *launches);
+/* While pass-1 timing is on, time one pass-1 launch in `every` (1, the default: all of them).
+ * Each timed launch carries start/stop events on its dispatch, which leave ~5 us of idle GPU
+ * behind it; a benchmark samples the launches to keep that out of most steps.  No sync. */
+int kbz_ctx_time_pass1_every(kbz_ctx_t *ctx, uint32_t every);
 /* The same for the pipeline's other stages (k_skip, k_chain, k_total, k_scan, k_resolve,
  * k_pack): stage_ms[KBZ_NSTAGES] gets each stage's summed duration over the batches timed since
  * the previous call (index KBZ_STAGE_*; pass 1 stays with kbz_ctx_time_pass1, slot 0 is 0),

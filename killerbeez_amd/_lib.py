@@ -31,6 +31,7 @@ SIGNATURES = [
     ("kbz_ctx_set_pass1", _i, [_vp, _i]),
     ("kbz_ctx_stats", _i, [_vp, _vp]),
     ("kbz_ctx_time_pass1", _i, [_vp, _i, C.POINTER(C.c_double), C.POINTER(_u32)]),
+    ("kbz_ctx_time_pass1_every", _i, [_vp, _u32]),
     ("kbz_ctx_time_stages", _i, [_vp, _i, _vp, C.POINTER(_u32)]),
     ("kbz_triage_batch_device", _i, [_vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _i, _vp]),
     ("kbz_triage_batch_host", _i, [_vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _i]),

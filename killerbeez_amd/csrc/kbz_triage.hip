@@ -3639,6 +3639,7 @@ struct kbz_ctx {
   uint32_t *h_err = nullptr, *d_err = nullptr;  // host-mapped copy of counters[1..2] (k_pack)
   // kbz_ctx_time_pass1: HIP events around every pass-1 launch (on its stream)
   bool timing = false;
+  uint32_t time_every = 1, p1_launch_no = 0;  // time one pass-1 launch in time_every
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pass1;
   size_t ev_used_n = 0;
   double pass1_folded_ms = 0;  // launches folded out of the event pool (kEvFoldAt)
@@ -3732,7 +3733,13 @@ constexpr int kWideD = KBZ_WIDE_D;          // their register ring depth
 constexpr uint32_t kWideBelowChunks = 512;  // 2 chunks per CU on a 256-CU MI355X
 // pass-1 / stage timing events: device-scope release (the default system-scope fence costs
 // ~6 us of idle GPU per event, profiles/r02_v9)
-constexpr unsigned kEventScope = hipEventReleaseToDevice;
+#ifndef KBZ_P1_STOP_ON_NEXT  // DynamoRIO pass-1 timing: stop event = k_skip's start (0: own stop)
+#define KBZ_P1_STOP_ON_NEXT 0
+#endif
+#ifndef KBZ_EVENT_FLAGS
+#define KBZ_EVENT_FLAGS hipEventReleaseToDevice
+#endif
+constexpr unsigned kEventScope = KBZ_EVENT_FLAGS;
 #ifndef KBZ_PASS1_DEPTH
 #define KBZ_PASS1_DEPTH 2
 #endif
@@ -4049,6 +4056,13 @@ int kbz_ctx_time_pass1(kbz_ctx_t *c, int enable, double *total_ms, uint32_t *lau
   c->timing = enable != 0;
   return 0;
 }
+int kbz_ctx_time_pass1_every(kbz_ctx_t *c, uint32_t every) {
+  if (!c) return fail("null ctx");
+  if (every == 0) return fail("every must be >= 1");
+  c->time_every = every;
+  c->p1_launch_no = 0;
+  return 0;
+}
 int kbz_ctx_time_stages(kbz_ctx_t *c, int enable, double *stage_ms, uint32_t *batches) {
   if (!c) return fail("null ctx");
   DevGuard g(c->device);
@@ -4169,7 +4183,7 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
     }
   }
   P1Ev pev;
-  if (c->timing) {
+  if (c->timing && (c->p1_launch_no++ % c->time_every) == 0) {
     if (c->ev_used_n >= kEvFoldAt && fold_pass1(c)) return -1;
     if (c->ev_used_n == c->ev_pass1.size()) {
       std::pair<hipEvent_t, hipEvent_t> e;
@@ -4182,7 +4196,13 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
     pev.start = c->ev_pass1[c->ev_used_n].first;
     pev.stop = c->ev_pass1[c->ev_used_n++].second;
   }
-  if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, hashed, s, pev)) return -1;
+  // DynamoRIO: pass 1's stop event is the start of k_skip, its successor on the stream (a stop
+  // event on pass 1's own dispatch left 4.8 us of idle GPU after it, profiles/r05_evgap; the
+  // interval now also holds the boundary, so the pass-1 time is an upper bound)
+  const bool stop_on_skip = pev.start && c->mode == KBZ_MODE_DYNAMORIO && KBZ_P1_STOP_ON_NEXT;
+  P1Ev pev1 = pev;
+  if (stop_on_skip) pev1.stop = nullptr;
+  if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, hashed, s, pev1)) return -1;
   if (c->mode == KBZ_MODE_DYNAMORIO) {  // the skip rule for rows j >= 1 needs no other shard
     hipEvent_t st0;
     if (stage_begin(c, s, &st0)) return -1;
@@ -4193,10 +4213,11 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
       if (fused_link(c, s, &x)) return -1;
       extra = 1 + x.copy_blocks;
     }
-    hipLaunchKernelGGL(k_skip, dim3(row_blocks + c->cur_chunks - 1 + extra), dim3(256), 0, s,
-                       c->cur_h32, c->neq, (uint32_t)n, c->skip, c->flags, c->fix_list,
-                       c->counters + 3, c->bad_list, c->counters + 4, c->shard_last, traces,
-                       stride, c->ignore, (uint32_t)c->M, row_blocks, x);
+    hipExtLaunchKernelGGL(k_skip, dim3(row_blocks + c->cur_chunks - 1 + extra), dim3(256), 0, s,
+                          stop_on_skip ? pev.stop : nullptr, nullptr, 0, c->cur_h32, c->neq,
+                          (uint32_t)n, c->skip, c->flags, c->fix_list, c->counters + 3,
+                          c->bad_list, c->counters + 4, c->shard_last, traces, stride, c->ignore,
+                          (uint32_t)c->M, row_blocks, x);
     HIP_TRY(hipGetLastError());
     if (fused) fused_link_commit(c);  // k_skip is queued: this batch's row is the next predecessor
     if (stage_end(c, s, KBZ_STAGE_SKIP, st0)) return -1;

@@ -78,6 +78,11 @@ class TriageContext:
               "kbz_ctx_time_pass1")
         return ms.value, k.value
 
+    def time_pass1_every(self, every: int) -> None:
+        """While pass-1 timing is on, time one launch in `every` (events on a dispatch leave ~5 us
+        of idle GPU behind it: a benchmark samples the launches).  No sync."""
+        check(lib().kbz_ctx_time_pass1_every(self._h, int(every)), "kbz_ctx_time_pass1_every")
+
     STAGES = ("pass1", "skip", "link", "reduce", "scan", "resolve", "pack")
 
     def time_stages(self, enable: bool = True):

@@ -31,3 +31,23 @@ def test_timers_fold_past_pool(gpu, staged, monkeypatch):
         # reading resets both
         assert ctx.time_pass1(False) == (0.0, 0)
         assert ctx.time_stages(False)[1] == 0
+
+
+def test_time_one_launch_in_every(gpu):
+    """kbz_ctx_time_pass1_every: 10 batches timed one in 4 -> launches 0, 4 and 8."""
+    m, n = 4096, 128
+    t, oc = synth.sparse_torch(n, m, device="cuda")
+    with TriageContext(m, MODE_DYNAMORIO, n) as ctx:
+        ctx.time_pass1_every(4)
+        ctx.time_pass1(True)
+        for _ in range(10):
+            ctx.triage(t, oc, WANT_H32)
+        torch.cuda.synchronize()
+        ms, launches = ctx.time_pass1(False)
+        assert launches == 3 and ms > 0
+        ctx.time_pass1_every(1)
+        ctx.time_pass1(True)
+        for _ in range(5):
+            ctx.triage(t, oc, WANT_H32)
+        torch.cuda.synchronize()
+        assert ctx.time_pass1(False)[1] == 5
