@@ -260,6 +260,35 @@ int kbz_merge_and_fill_devices(uint8_t *out, size_t n, size_t state_bytes, kbz_m
                                void *user, const int *devices, size_t ndev, int exchange,
                                int *used_out);
 
+/* ---- sharded triage over the GPUs of one node, from C ---------------------------------------- */
+/* BASELINE north_star "Batches shard across the 8 GPUs of one node" for a C caller of the batched
+ * loop (fuzzer/main.c:370-418 through INTEGRATION.md §2), in one process: the sharded protocol
+ * above (kbz_shard_*) driven over ndev workers, worker w a context on device devices[w] (a device
+ * may repeat: several workers on one GPU).  kbz_triage_batch_devices splits a HOST batch of n
+ * traces (row i at traces + i*stride, stride >= map_size; outcome host int8[n] or NULL) into
+ * contiguous shards [n*w/ndev, n*(w+1)/ndev), each at most max_batch; copies each to its
+ * worker's device; runs pass 1 there; (DynamoRIO) gathers every shard's last row and hash pair on
+ * every worker and links; gathers the shards' OR aggregates on every worker (peer copies, or
+ * device-local copies for workers sharing a GPU: RCCL has no bitwise reduction, and one process
+ * needs no communicator) and resolves with the prefix of the earlier shards.  hnb_out (host
+ * uint8[n], or NULL) and h32_out (host uint32[n], or NULL; DynamoRIO always hashes) get the
+ * results of one sequential pass over the whole batch -- the reference's per-exec
+ * has_new_bits / has_new_coverage -- and every worker's virgin maps and last hash become that
+ * pass's.  XXH64 is not offered here (KBZ_WANT_X64 fails).  Synchronous. */
+typedef struct kbz_mctx kbz_mctx_t;
+kbz_mctx_t *kbz_mctx_create(size_t map_size, int mode, size_t max_batch, const int *devices,
+                            size_t ndev);
+void kbz_mctx_destroy(kbz_mctx_t *m);
+int kbz_mctx_workers(kbz_mctx_t *m);
+kbz_ctx_t *kbz_mctx_worker(kbz_mctx_t *m, size_t w);  /* its context (ignore bytes, stats) */
+int kbz_triage_batch_devices(kbz_mctx_t *m, const uint8_t *traces, size_t n, size_t stride,
+                             const int8_t *outcome, uint8_t *hnb_out, uint32_t *h32_out,
+                             int want);
+/* Worker 0's virgin maps / last hash (every worker holds the same); set_virgin sets all. */
+int kbz_mctx_get_virgin(kbz_mctx_t *m, uint8_t *host_out);
+int kbz_mctx_set_virgin(kbz_mctx_t *m, const uint8_t *host_in);
+int kbz_mctx_get_last_hash(kbz_mctx_t *m, uint32_t *out);
+
 /* ---- DynamoRIO per-module coverage ----------------------------------------------------------- */
 /* has_new_coverage_per_module (dynamorio_instrumentation.c:1477-1493) over an ordered batch: each
  * traced module m has its own context ctxs[m] (its virgin map, ignore bytes and last hash, as

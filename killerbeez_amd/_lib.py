@@ -53,6 +53,14 @@ SIGNATURES = [
     ("kbz_merge_and_fill", _i, [_vp, _sz, _sz, _vp, _vp]),
     ("kbz_merge_and_fill_device", _i, [_vp, _sz, _sz, _vp, _vp, _vp]),
     ("kbz_merge_and_fill_devices", _i, [_vp, _sz, _sz, _vp, _vp, _vp, _sz, _i, C.POINTER(_i)]),
+    ("kbz_mctx_create", _vp, [_sz, _i, _sz, _vp, _sz]),
+    ("kbz_mctx_destroy", None, [_vp]),
+    ("kbz_mctx_workers", _i, [_vp]),
+    ("kbz_mctx_worker", _vp, [_vp, _sz]),
+    ("kbz_triage_batch_devices", _i, [_vp, _vp, _sz, _sz, _vp, _vp, _vp, _i]),
+    ("kbz_mctx_get_virgin", _i, [_vp, _vp]),
+    ("kbz_mctx_set_virgin", _i, [_vp, _vp]),
+    ("kbz_mctx_get_last_hash", _i, [_vp, C.POINTER(_u32)]),
     ("kbz_triage_modules_device", _i, [_vp, _sz, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("kbz_triage_modules_host", _i, [_vp, _sz, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp]),
     ("kbz_transform_rows_device", _i, [_vp, _sz, _sz, _sz, _i, _vp, _sz, _vp]),

@@ -272,3 +272,232 @@ extern "C" int kbz_merge_and_fill_devices(uint8_t *out, size_t n, size_t state_b
   }
   return 0;
 }
+
+// ---- sharded triage over several GPUs of one node, from C -----------------------------------
+// The protocol of killerbeez_amd/dist.py (include/kbz_triage.h "sharded
+// triage") driven by one host thread over W workers, each a kbz_ctx on its device with its own
+// stream: contiguous shards of a host batch, the DynamoRIO link rows and the OR aggregates
+// exchanged by peer copies (device-local copies for workers sharing a GPU) into a gather buffer
+// on every worker, one kbz_or_prefix_total per worker.  Cross-stream order by events only: no
+// host sync until the results are copied back.
+struct kbz_mctx {
+  size_t M = 0, max_batch = 0, W = 0, ab = 0;  // ab = aggregate bytes per worker
+  int mode = 0;
+  std::vector<int> dev;
+  std::vector<kbz_ctx_t *> ctx;
+  std::vector<hipStream_t> s;
+  std::vector<hipEvent_t> ev_link, ev_agg;
+  std::vector<uint8_t *> traces, hnb, mine, gather, agg_mine, agg_all, prefix, total;
+  std::vector<int8_t *> oc;
+  std::vector<uint32_t *> h32;
+};
+
+namespace {
+void mctx_free(kbz_mctx *m) {
+  for (size_t w = 0; w < m->W; w++) {
+    if (w < m->dev.size()) (void)hipSetDevice(m->dev[w]);
+    if (w < m->s.size() && m->s[w]) (void)hipStreamSynchronize(m->s[w]);
+    for (auto *v : {&m->traces, &m->hnb, &m->mine, &m->gather, &m->agg_mine, &m->agg_all,
+                    &m->prefix, &m->total})
+      if (w < v->size() && (*v)[w]) (void)hipFree((*v)[w]);
+    if (w < m->oc.size() && m->oc[w]) (void)hipFree(m->oc[w]);
+    if (w < m->h32.size() && m->h32[w]) (void)hipFree(m->h32[w]);
+    if (w < m->ev_link.size() && m->ev_link[w]) (void)hipEventDestroy(m->ev_link[w]);
+    if (w < m->ev_agg.size() && m->ev_agg[w]) (void)hipEventDestroy(m->ev_agg[w]);
+    if (w < m->ctx.size() && m->ctx[w]) kbz_ctx_destroy(m->ctx[w]);
+    if (w < m->s.size() && m->s[w]) (void)hipStreamDestroy(m->s[w]);
+  }
+  delete m;
+}
+// dst (on device dd) <- src (on device sd), n bytes, on stream st (dd's)
+hipError_t xcopy(void *dst, int dd, const void *src, int sd, size_t n, hipStream_t st) {
+  if (dd == sd) return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, st);
+  return hipMemcpyPeerAsync(dst, dd, src, sd, n, st);
+}
+}  // namespace
+
+extern "C" kbz_mctx_t *kbz_mctx_create(size_t map_size, int mode, size_t max_batch,
+                                       const int *devices, size_t ndev) {
+  if (!devices || ndev == 0) {
+    fail_multi("kbz_mctx_create: devices[] and ndev >= 1 are required");
+    return nullptr;
+  }
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess) {
+    fail_multi("kbz_mctx_create: no device");
+    return nullptr;
+  }
+  for (size_t w = 0; w < ndev; w++)
+    if (devices[w] < 0 || devices[w] >= count) {
+      fail_multi("kbz_mctx_create: device ordinal out of range");
+      return nullptr;
+    }
+  DevScope keep;
+  kbz_mctx *m = new kbz_mctx;
+  m->M = map_size;
+  m->mode = mode;
+  m->max_batch = max_batch;
+  m->W = ndev;
+  m->dev.assign(devices, devices + ndev);
+  const size_t W = ndev, row = map_size + 16;  // gathered link rows: [row | hash pair | pad]
+  for (auto *v : {&m->traces, &m->hnb, &m->mine, &m->gather, &m->agg_mine, &m->agg_all,
+                  &m->prefix, &m->total})
+    v->assign(W, nullptr);
+  m->oc.assign(W, nullptr);
+  m->h32.assign(W, nullptr);
+  m->ctx.assign(W, nullptr);
+  m->s.assign(W, nullptr);
+  m->ev_link.assign(W, nullptr);
+  m->ev_agg.assign(W, nullptr);
+  auto bad = [&](const char *what) {
+    std::string msg = std::string("kbz_mctx_create: ") + what;
+    mctx_free(m);
+    fail_multi(msg);
+    return (kbz_mctx_t *)nullptr;
+  };
+  for (size_t w = 0; w < W; w++) {
+    if (hipSetDevice(m->dev[w]) != hipSuccess) return bad("hipSetDevice");
+    m->ctx[w] = kbz_ctx_create(map_size, mode, max_batch);
+    if (!m->ctx[w]) return bad(kbz_last_error());
+    if (w == 0) m->ab = kbz_shard_aggregate_bytes(m->ctx[0]);
+    if (hipStreamCreateWithFlags(&m->s[w], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_link[w], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_agg[w], hipEventDisableTiming) != hipSuccess ||
+        hipMalloc((void **)&m->traces[w], max_batch * map_size + 16) != hipSuccess ||
+        hipMalloc((void **)&m->oc[w], max_batch + 16) != hipSuccess ||
+        hipMalloc((void **)&m->h32[w], max_batch * 4 + 16) != hipSuccess ||
+        hipMalloc((void **)&m->hnb[w], max_batch + 16) != hipSuccess ||
+        hipMalloc((void **)&m->mine[w], row) != hipSuccess ||
+        hipMalloc((void **)&m->gather[w], W * row) != hipSuccess ||
+        hipMalloc((void **)&m->agg_mine[w], m->ab) != hipSuccess ||
+        hipMalloc((void **)&m->agg_all[w], W * m->ab) != hipSuccess ||
+        hipMalloc((void **)&m->prefix[w], m->ab) != hipSuccess ||
+        hipMalloc((void **)&m->total[w], m->ab) != hipSuccess)
+      return bad("out of device memory");
+    if (hipMemset(m->mine[w], 0, row) != hipSuccess) return bad("hipMemset");
+  }
+  return m;
+}
+
+extern "C" void kbz_mctx_destroy(kbz_mctx_t *m) {
+  if (!m) return;
+  DevScope keep;
+  mctx_free(m);
+}
+
+extern "C" int kbz_mctx_workers(kbz_mctx_t *m) { return m ? (int)m->W : -1; }
+extern "C" kbz_ctx_t *kbz_mctx_worker(kbz_mctx_t *m, size_t w) {
+  return (m && w < m->W) ? m->ctx[w] : nullptr;
+}
+
+extern "C" int kbz_triage_batch_devices(kbz_mctx_t *m, const uint8_t *traces, size_t n,
+                                        size_t stride, const int8_t *outcome, uint8_t *hnb_out,
+                                        uint32_t *h32_out, int want) {
+  if (!m) return fail_multi("null mctx");
+  if (n && (!traces || stride < m->M)) return fail_multi("bad traces / stride");
+  if (want & KBZ_WANT_X64) return fail_multi("kbz_triage_batch_devices: XXH64 is not gathered");
+  const size_t W = m->W, M = m->M, row = M + 16;
+  std::vector<size_t> lo(W + 1);
+  for (size_t w = 0; w <= W; w++) lo[w] = n * w / W;
+  for (size_t w = 0; w < W; w++)
+    if (lo[w + 1] - lo[w] > m->max_batch) return fail_multi("a shard exceeds max_batch");
+  DevScope keep;
+  const bool dr = m->mode == KBZ_MODE_DYNAMORIO;
+  const bool hashed = dr || (want & KBZ_WANT_H32);
+  std::vector<size_t> nonempty;
+  for (size_t w = 0; w < W; w++)
+    if (lo[w + 1] > lo[w]) nonempty.push_back(w);
+  // 1. shards to their devices, pass 1 (+ k_skip); DynamoRIO: each shard's link row and hash pair
+  for (size_t w = 0; w < W; w++) {
+    const size_t nw = lo[w + 1] - lo[w];
+    MHIP(hipSetDevice(m->dev[w]));
+    if (nw) {
+      MHIP(hipMemcpy2DAsync(m->traces[w], M, traces + lo[w] * stride, stride, M, nw,
+                            hipMemcpyHostToDevice, m->s[w]));
+      if (outcome)
+        MHIP(hipMemcpyAsync(m->oc[w], outcome + lo[w], nw, hipMemcpyHostToDevice, m->s[w]));
+    }
+    if (kbz_shard_begin(m->ctx[w], nw ? m->traces[w] : nullptr, nw, M, outcome ? m->oc[w] : nullptr,
+                        hashed ? m->h32[w] : nullptr, nullptr, want, m->s[w]))
+      return -1;
+    if (dr) {
+      if (kbz_shard_last_row(m->ctx[w], m->mine[w], m->s[w]) ||
+          kbz_shard_last_hash(m->ctx[w], (uint32_t *)(m->mine[w] + M), m->s[w]))
+        return -1;
+      MHIP(hipEventRecord(m->ev_link[w], m->s[w]));
+    }
+  }
+  // 2. DynamoRIO: every worker gathers the link rows, then links to the nearest non-empty earlier
+  //    shard and to the last non-empty one (the batch's last exec)
+  for (size_t v = 0; v < W; v++) {
+    MHIP(hipSetDevice(m->dev[v]));
+    if (dr) {
+      for (size_t w : nonempty) {
+        MHIP(hipStreamWaitEvent(m->s[v], m->ev_link[w], 0));
+        MHIP(xcopy(m->gather[v] + w * row, m->dev[v], m->mine[w], m->dev[w], row, m->s[v]));
+      }
+      long p = -1;
+      for (size_t w : nonempty)
+        if (w < v) p = (long)w;
+      const long g = nonempty.empty() ? -1 : (long)nonempty.back();
+      const uint8_t *gp = m->gather[v];
+      if (kbz_shard_link(m->ctx[v], p < 0 ? nullptr : (const uint32_t *)(gp + p * row + M),
+                         p < 0 ? nullptr : gp + p * row, p < 0 ? 1 : 0,
+                         g < 0 ? nullptr : (const uint32_t *)(gp + g * row + M),
+                         g < 0 ? nullptr : gp + g * row, m->s[v]))
+        return -1;
+    } else if (kbz_shard_link(m->ctx[v], nullptr, nullptr, 1, nullptr, nullptr, m->s[v])) {
+      return -1;
+    }
+    if (kbz_shard_reduce(m->ctx[v], m->s[v]) ||
+        kbz_shard_aggregate(m->ctx[v], m->agg_mine[v], m->s[v]))
+      return -1;
+    MHIP(hipEventRecord(m->ev_agg[v], m->s[v]));
+  }
+  // 3. every worker gathers the aggregates: prefix (earlier shards) and total; resolve; results
+  for (size_t v = 0; v < W; v++) {
+    MHIP(hipSetDevice(m->dev[v]));
+    for (size_t w = 0; w < W; w++) {
+      MHIP(hipStreamWaitEvent(m->s[v], m->ev_agg[w], 0));
+      MHIP(xcopy(m->agg_all[v] + w * m->ab, m->dev[v], m->agg_mine[w], m->dev[w], m->ab, m->s[v]));
+    }
+    if (kbz_or_prefix_total(v ? m->prefix[v] : nullptr, m->total[v], m->agg_all[v], v, W, m->ab,
+                            m->s[v]) ||
+        kbz_shard_finish(m->ctx[v], v ? m->prefix[v] : nullptr, m->total[v], m->hnb[v], m->s[v]))
+      return -1;
+    const size_t nw = lo[v + 1] - lo[v];
+    if (nw && hnb_out)
+      MHIP(hipMemcpyAsync(hnb_out + lo[v], m->hnb[v], nw, hipMemcpyDeviceToHost, m->s[v]));
+    if (nw && h32_out && hashed)
+      MHIP(hipMemcpyAsync(h32_out + lo[v], m->h32[v], nw * 4, hipMemcpyDeviceToHost, m->s[v]));
+  }
+  for (size_t v = 0; v < W; v++) {
+    MHIP(hipSetDevice(m->dev[v]));
+    if (kbz_sync(m->ctx[v], m->s[v])) return -1;  // the stream, then the sticky error flags
+  }
+  return 0;
+}
+
+extern "C" int kbz_mctx_get_virgin(kbz_mctx_t *m, uint8_t *host_out) {
+  if (!m || !host_out) return fail_multi("null argument");
+  DevScope keep;
+  MHIP(hipSetDevice(m->dev[0]));
+  return kbz_get_virgin(m->ctx[0], host_out);
+}
+
+extern "C" int kbz_mctx_set_virgin(kbz_mctx_t *m, const uint8_t *host_in) {
+  if (!m || !host_in) return fail_multi("null argument");
+  DevScope keep;
+  for (size_t w = 0; w < m->W; w++) {
+    MHIP(hipSetDevice(m->dev[w]));
+    if (kbz_set_virgin(m->ctx[w], host_in)) return -1;
+  }
+  return 0;
+}
+
+extern "C" int kbz_mctx_get_last_hash(kbz_mctx_t *m, uint32_t *out) {
+  if (!m || !out) return fail_multi("null argument");
+  DevScope keep;
+  MHIP(hipSetDevice(m->dev[0]));
+  return kbz_get_last_hash(m->ctx[0], out);
+}

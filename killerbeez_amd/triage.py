@@ -362,6 +362,70 @@ def merge_and_devices(states: np.ndarray, devices=None, exchange: int = EXCHANGE
     return out, used.value
 
 
+class MultiTriageContext:
+    """Sharded triage over several GPUs of one node from C (kbz_mctx_*,
+    kbz_triage_batch_devices): worker w is a context on devices[w] (a device may repeat); a host
+    batch is split into contiguous shards, one per worker, and the results are those of one
+    sequential pass over the whole batch (the reference's per-exec has_new_bits)."""
+
+    def __init__(self, map_size: int = 65536, mode: int | str = MODE_AFL,
+                 max_batch: int = 65536, devices=(0,)):
+        if isinstance(mode, str):
+            mode = MODES[mode]
+        self.map_size, self.mode = map_size, mode
+        arr = (C.c_int * len(devices))(*devices)
+        self._h = lib().kbz_mctx_create(map_size, mode, max_batch, C.cast(arr, C.c_void_p),
+                                        len(devices))
+        if not self._h:
+            raise KbzError((lib().kbz_last_error() or b"kbz_mctx_create failed").decode())
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().kbz_mctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def workers(self) -> int:
+        return lib().kbz_mctx_workers(self._h)
+
+    def triage_host(self, traces: np.ndarray, outcome=None, want: int = WANT_H32):
+        t = np.ascontiguousarray(traces, dtype=np.uint8)
+        n = t.shape[0]
+        hnb = np.zeros(n, np.uint8)
+        h32 = np.zeros(n, np.uint32)
+        oc = None if outcome is None else np.ascontiguousarray(outcome, dtype=np.int8)
+        check(lib().kbz_triage_batch_devices(self._h, _np_ptr(t) if n else None, n, self.map_size,
+                                             None if oc is None else _np_ptr(oc), _np_ptr(hnb),
+                                             _np_ptr(h32), want), "kbz_triage_batch_devices")
+        return {"hnb": hnb, "h32": h32}
+
+    def get_virgin(self) -> np.ndarray:
+        v = np.empty((3, self.map_size), np.uint8)
+        check(lib().kbz_mctx_get_virgin(self._h, _np_ptr(v)), "kbz_mctx_get_virgin")
+        return v
+
+    def set_virgin(self, v: np.ndarray) -> None:
+        v = np.ascontiguousarray(v, dtype=np.uint8)
+        check(lib().kbz_mctx_set_virgin(self._h, _np_ptr(v)), "kbz_mctx_set_virgin")
+
+    @property
+    def last_hash(self) -> int:
+        out = C.c_uint32()
+        check(lib().kbz_mctx_get_last_hash(self._h, C.byref(out)), "kbz_mctx_get_last_hash")
+        return out.value
+
+
 def triage_modules(ctxs, traces, offsets, outcome=None, stream=None, hashes=False):
     """DynamoRIO per-module coverage (has_new_coverage_per_module,
     dynamorio_instrumentation.c:1477-1493) over an ordered batch.  ctxs: one TriageContext per

@@ -1,0 +1,85 @@
+"""Sharded triage over several GPUs of one node from C (kbz_mctx_*, kbz_triage_batch_devices;
+include/kbz_triage.h): the protocol of killerbeez_amd.dist in one process,
+workers exchanging link rows and OR aggregates by peer / device-local copies.  On a one-GPU box
+the workers share cuda:0 (several contexts, device-local copies); the results must equal one
+sequential pass of the CPU oracle over the whole batch, batch after batch (virgin maps and the
+DynamoRIO last hash carried), with ragged and empty shards and repeats across shard boundaries."""
+import numpy as np
+import pytest
+
+import oracle
+from killerbeez_amd import synth
+from killerbeez_amd.triage import WANT_H32, KbzError, MultiTriageContext
+
+MODES = [0, 1, 2]
+
+
+def _sharded_batches(mode, devices):
+    m = 4096
+    sizes = [700, 1001, 2, 0, 333]  # ragged shards; 2 and 0 traces leave workers empty
+    v = np.full((3, m), 0xFF, np.uint8)
+    last = 0
+    with MultiTriageContext(m, mode, 512, devices=devices) as mc:
+        assert mc.workers() == len(devices)
+        for b, n in enumerate(sizes):
+            t, oc = synth.sparse_np(n, m, seed=500 + 31 * b + mode, hot_frac=0.05)
+            if n > 10:
+                cut = n // len(devices)  # a repeat across the first shard boundary (DynamoRIO skip)
+                t[cut] = t[cut - 1]
+                t[n // 2 + 1] = t[n // 2]
+            exp = oracle.triage_batch(mode, t, oc, virgin=v, last_hash=last, want=oracle.WANT_H32)
+            got = mc.triage_host(t, oc, WANT_H32)
+            np.testing.assert_array_equal(got["hnb"], exp["hnb"])
+            if mode == 1 or n:
+                np.testing.assert_array_equal(got["h32"], exp["h32"])
+            np.testing.assert_array_equal(mc.get_virgin(), exp["virgin"])
+            if mode == 1:
+                assert mc.last_hash == exp["last_hash"]
+            v, last = exp["virgin"], exp.get("last_hash", last)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("workers", [2, 3])
+def test_sharded_batches_from_c(gpu, mode, workers):
+    """Workers sharing cuda:0 (device-local copies)."""
+    _sharded_batches(mode, [0] * workers)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", MODES)
+def test_sharded_batches_from_c_distinct_gpus(gpu, mode):
+    """One worker per GPU (peer copies over xGMI); needs a multi-GPU node."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs >= 2 GPUs")
+    _sharded_batches(mode, list(range(min(torch.cuda.device_count(), 4))))
+
+
+@pytest.mark.gpu
+def test_sharded_from_c_set_virgin_and_limits(gpu):
+    m = 2048
+    t, oc = synth.sparse_np(300, m, seed=9, hot_frac=0.05)
+    with MultiTriageContext(m, 1, 100, devices=[0, 0]) as mc:
+        pre = np.full((3, m), 0xFF, np.uint8)
+        pre[0, : m // 2] = 0  # a preset map reaches every worker
+        mc.set_virgin(pre)
+        with pytest.raises(KbzError, match="max_batch"):
+            mc.triage_host(t, oc)  # 150 traces per worker > 100
+        got = mc.triage_host(t[:200], oc[:200])
+        exp = oracle.triage_batch(1, t[:200], oc[:200], virgin=pre, want=oracle.WANT_H32)
+        np.testing.assert_array_equal(got["hnb"], exp["hnb"])
+        np.testing.assert_array_equal(mc.get_virgin(), exp["virgin"])
+    with pytest.raises(KbzError, match="out of range"):
+        MultiTriageContext(m, 1, 100, devices=[0, 999])
+
+
+def test_mctx_create_fails_loudly_without_a_device():
+    """On a host with no GPU the multi-device context refuses to start (no CPU fallback)."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(KbzError, match="no device"):
+        MultiTriageContext(1024, 0, 16, devices=[0])
