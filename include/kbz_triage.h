@@ -92,6 +92,10 @@ int kbz_set_ignore(kbz_ctx_t *ctx, const uint8_t *host_ignore);
  * virgin_crash.  DYNAMORIO mode uses only virgin_bits.  Synchronous. */
 int kbz_get_virgin(kbz_ctx_t *ctx, uint8_t *host_out);
 int kbz_set_virgin(kbz_ctx_t *ctx, const uint8_t *host_in);
+/* Stream-ordered reset of the three virgin maps to all-0xff, as a fresh afl_state_t or the
+ * DynamoRIO plugin's first enable (dynamorio_instrumentation.c:496-497): no host sync; the next
+ * batch enqueued on `stream` (or ordered after it) sees fresh maps. */
+int kbz_reset_virgin(kbz_ctx_t *ctx, void *stream);
 /* DynamoRIO last_shm_hash (dynamorio_instrumentation.c:1450-1461).  Synchronous.  The context
  * also keeps the previous batch's last trace (to tell a repeated exec from a hash collision);
  * kbz_set_last_hash forgets it, so a restored hash is handled without it (still exact). */

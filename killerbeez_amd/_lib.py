@@ -25,6 +25,7 @@ SIGNATURES = [
     ("kbz_set_ignore", _i, [_vp, _vp]),
     ("kbz_get_virgin", _i, [_vp, _vp]),
     ("kbz_set_virgin", _i, [_vp, _vp]),
+    ("kbz_reset_virgin", _i, [_vp, _vp]),
     ("kbz_get_last_hash", _i, [_vp, C.POINTER(_u32)]),
     ("kbz_set_last_hash", _i, [_vp, _u32]),
     ("kbz_virgin_device", _vp, [_vp]),

@@ -4023,6 +4023,14 @@ int kbz_set_virgin(kbz_ctx_t *c, const uint8_t *in) {
   c->saved_valid = false;
   return 0;
 }
+int kbz_reset_virgin(kbz_ctx_t *c, void *stream) {
+  if (!c) return fail("null argument");
+  DevGuard g(c->device);
+  // the buffer the next enqueued batch reads (vcur flips when a batch is enqueued)
+  HIP_TRY(hipMemsetAsync(c->V[c->vcur], 0xff, 3 * c->M, (hipStream_t)stream));
+  c->saved_valid = false;  // as kbz_set_virgin: the saved row's bits may not be in the new maps
+  return 0;
+}
 int kbz_get_last_hash(kbz_ctx_t *c, uint32_t *out) {
   if (!c || !out) return fail("null argument");
   DevGuard g(c->device);

@@ -126,6 +126,10 @@ class TriageContext:
         v = np.ascontiguousarray(v, dtype=np.uint8).reshape(3, self.map_size)
         check(lib().kbz_set_virgin(self._h, _np_ptr(v)), "kbz_set_virgin")
 
+    def reset_virgin(self, stream=None) -> None:
+        """All-0xff virgin maps for the next batch on `stream`, stream-ordered (no host sync)."""
+        check(lib().kbz_reset_virgin(self._h, _stream_handle(stream)), "kbz_reset_virgin")
+
     @property
     def last_hash(self) -> int:
         x = C.c_uint32()

@@ -726,6 +726,40 @@ def test_set_virgin_after_a_batch_forgets_the_saved_row(gpu):
     ctx.close()
 
 
+@pytest.mark.parametrize("mode", MODES)
+def test_reset_virgin_is_stream_ordered(gpu, mode):
+    """kbz_reset_virgin between two batches enqueued back to back (no host sync): the second
+    batch sees all-0xff maps, the DynamoRIO last hash carries over, and its first rows repeat
+    the first batch's last row (a skip, then a changed copy that is new again)."""
+    import torch
+
+    m = 4096
+    t, oc = synth.sparse_np(300, m, seed=2031 + mode, hot_frac=0.05)
+    a, b = t[:150].copy(), t[150:].copy()
+    b[0] = a[-1]
+    b[1] = a[-1]
+    b[1, 11] ^= 0x02
+    fresh = np.full((3, m), 0xFF, np.uint8)
+    exp_a = oracle.triage_batch(mode, a, oc[:150], virgin=fresh, want=oracle.WANT_H32)
+    exp_b = oracle.triage_batch(mode, b, oc[150:], virgin=fresh, last_hash=exp_a["last_hash"],
+                                want=oracle.WANT_H32)
+    with TriageContext(m, mode, 150) as ctx:
+        ta, tb = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+        oa, ob = torch.from_numpy(oc[:150]).cuda(), torch.from_numpy(oc[150:]).cuda()
+        ra = ctx.triage(ta, oa, WANT_H32)
+        ctx.reset_virgin()
+        rb = ctx.triage(tb, ob, WANT_H32)
+        torch.cuda.synchronize()
+        ctx.sync()
+        np.testing.assert_array_equal(ra["hnb"].cpu().numpy(), exp_a["hnb"])
+        np.testing.assert_array_equal(rb["hnb"].cpu().numpy(), exp_b["hnb"])
+        np.testing.assert_array_equal(rb["h32"].cpu().numpy().view(np.uint32), exp_b["h32"])
+        np.testing.assert_array_equal(ctx.get_virgin(), exp_b["virgin"])
+        if mode == MODE_DYNAMORIO:
+            assert ctx.last_hash == exp_b["last_hash"]
+            assert exp_b["hnb"][0] == 0 and exp_b["hnb"][1] > 0
+
+
 def test_claim_overflow_is_reported_once(gpu, monkeypatch):
     """A claim-list overflow (forced with a tiny debug list) fails that batch once: the next
     ring acquire / record works and later batches are exact again."""
