@@ -250,22 +250,28 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 // tools/tail_stamps.py through kbz_debug_tail().  No record is written otherwise.
 #ifdef KBZ_TAIL_STAMPS
 constexpr int kTailRecs = 1 << 16;
-__device__ unsigned long long g_kbz_tail[kTailRecs * 4];
+constexpr int kTailFields = 8;  // t0, prologue end, end, work counters, 4 phase sums (k_tail)
+__device__ unsigned long long g_kbz_tail[kTailRecs * kTailFields];
 __device__ __forceinline__ unsigned long long rt_now() {
   unsigned long long t;
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
   return t;
 }
-#define KBZ_TAIL_DECL unsigned long long tl_t0 = rt_now(), tl_t1 = 0; uint32_t tl_walk = 0, tl_claims = 0, tl_flush = 0, tl_win = 0
-#define KBZ_TAIL_MARK() (tl_t1 = rt_now())
+#define KBZ_TAIL_DECL unsigned long long tl_t0 = rt_now(), tl_t1 = 0, tl_last = 0, tl_ph[4] = {0, 0, 0, 0}; uint32_t tl_walk = 0, tl_claims = 0, tl_flush = 0, tl_win = 0
+#define KBZ_TAIL_MARK() (tl_t1 = tl_last = rt_now())
 #define KBZ_TAIL_ADD(f, v) (tl_##f += (v))
+// phase sums of k_tail's walk (the stamp build waits for every load at each phase end, so a
+// phase's loads are charged to it): 0 group loads, 1 per-chunk claims, 2 record scores, 3 flushes
+#define KBZ_TAIL_PH(i) do { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); const unsigned long long _n = rt_now(); tl_ph[i] += _n - tl_last; tl_last = _n; } while (0)
 #define KBZ_TAIL_END(id) do { const unsigned long long _e = rt_now(); const uint32_t _i = (id); \
-    if ((threadIdx.x & 63) == 0 && _i < (uint32_t)kTailRecs) { g_kbz_tail[_i * 4] = tl_t0; g_kbz_tail[_i * 4 + 1] = tl_t1 ? tl_t1 : _e; \
-    g_kbz_tail[_i * 4 + 2] = _e; g_kbz_tail[_i * 4 + 3] = ((unsigned long long)tl_walk << 48) | ((unsigned long long)(tl_claims & 0xffff) << 32) | ((tl_flush & 0xffff) << 16) | (tl_win & 0xffff); } } while (0)
+    if ((threadIdx.x & 63) == 0 && _i < (uint32_t)kTailRecs) { unsigned long long *_r = g_kbz_tail + (size_t)_i * kTailFields; _r[0] = tl_t0; _r[1] = tl_t1 ? tl_t1 : _e; \
+    _r[2] = _e; _r[3] = ((unsigned long long)tl_walk << 48) | ((unsigned long long)(tl_claims & 0xffff) << 32) | ((tl_flush & 0xffff) << 16) | (tl_win & 0xffff); \
+    for (int _p = 0; _p < 4; _p++) _r[4 + _p] = tl_ph[_p]; } } while (0)
 #else
 #define KBZ_TAIL_DECL do {} while (0)
 #define KBZ_TAIL_MARK() do {} while (0)
 #define KBZ_TAIL_ADD(f, v) do {} while (0)
+#define KBZ_TAIL_PH(i) do {} while (0)
 #define KBZ_TAIL_END(id) do {} while (0)
 #endif
 __device__ __forceinline__ void lds_barrier() {
@@ -2948,6 +2954,7 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
             ri[u] = 0;
             rv[u] = 0;
           }
+          KBZ_TAIL_PH(0);
 #pragma unroll
           for (int u = 0; u < KBZ_SCAN_ILP; u++) {
             const uint32_t c = cs[u];  // uniform across the wave
@@ -3001,13 +3008,16 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
             }
             prev = or4(prev, o[u]);
           }
+          KBZ_TAIL_PH(1);
 #pragma unroll
           for (int u = 0; u < KBZ_SCAN_ILP; u++)
             if (ri[u] >> 16) record_score(rv[u], ri[u], cs[u], a.epoch, a.ca.hnb32, a.ca.err);
+          KBZ_TAIL_PH(2);
         }
       }
       claims_flush(a.ca, cq);
       flush_items(stg, a.items, a.cap, a.counters);
+      KBZ_TAIL_PH(3);
     }
   }
   KBZ_TAIL_END(tail_id);
@@ -4584,10 +4594,10 @@ int kbz_or_reduce(uint8_t *out, const uint8_t *in, size_t r_lo, size_t r_hi, siz
 int kbz_debug_tail(unsigned long long *host_out, size_t count) {
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_kbz_tail),
-                              std::min<size_t>(count, (size_t)kTailRecs * 4) * 8));
+                              std::min<size_t>(count, (size_t)kTailRecs * kTailFields) * 8));
   void *sym = nullptr;
   HIP_TRY(hipGetSymbolAddress(&sym, HIP_SYMBOL(g_kbz_tail)));
-  HIP_TRY(hipMemset(sym, 0, (size_t)kTailRecs * 4 * 8));
+  HIP_TRY(hipMemset(sym, 0, (size_t)kTailRecs * kTailFields * 8));
   return 0;
 }
 #endif

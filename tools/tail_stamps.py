@@ -26,7 +26,8 @@ f = L.kbz_debug_tail
 f.restype = C.c_int
 f.argtypes = [C.c_void_p, C.c_size_t]
 NREC = 1 << 16
-buf = np.zeros(NREC * 4, np.uint64)
+NF = 8  # fields per wave record (kTailFields)
+buf = np.zeros(NREC * NF, np.uint64)
 dev = torch.device("cuda:0")
 mode = MODES[mode_name]
 want = WANT_H32 if mode == MODES["dynamorio"] else 0
@@ -45,8 +46,8 @@ with TriageContext(M, mode, B) as ctx:
         ctx.triage(t, oc, want, out=out)
         torch.cuda.synchronize()
         ctx.sync()
-        assert f(buf.ctypes.data, NREC * 4) == 0
-        r = buf.reshape(NREC, 4)
+        assert f(buf.ctypes.data, NREC * NF) == 0
+        r = buf.reshape(NREC, NF)
         live = r[r[:, 0] != 0]
         t0 = live[:, 0].astype(np.int64)
         t1 = live[:, 1].astype(np.int64)
@@ -55,6 +56,7 @@ with TriageContext(M, mode, B) as ctx:
         walk = (cnt >> 48) & 0xFFFF
         claims = (cnt >> 32) & 0xFFFF
         win = cnt & 0xFFFF
+        ph = live[:, 4:8].astype(np.float64) / 100.0
         base = t0.min()
         dur = (t2 - t0) / 100.0  # us (100 MHz)
         order = np.argsort(-dur)
@@ -68,7 +70,11 @@ with TriageContext(M, mode, B) as ctx:
                                     for q in (50, 100)],
             "walk_total": int(walk.sum()), "claims_total": int(claims.sum()),
             "windows_total": int(win.sum()),
+            # k_tail walk phases (us): group loads, per-chunk claims, record scores, flushes
+            "phase_us_p50": [round(float(np.percentile(ph[:, p], 50)), 2) for p in range(4)],
             "slowest": [{"dur_us": round(float(dur[j]), 2), "start_us": round((t0[j] - base) / 100.0, 2),
+                         "prologue_us": round((t1[j] - t0[j]) / 100.0, 2),
+                         "phase_us": [round(float(x), 2) for x in ph[j]],
                          "walk": int(walk[j]), "claims": int(claims[j]), "win": int(win[j])}
                         for j in order[:6]],
         }
