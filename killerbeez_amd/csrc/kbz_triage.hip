@@ -389,6 +389,18 @@ struct Pass1Args {
                         // bytes / XXH64, one-shard batches) or null
   uint64_t *rflags;     // [chunks][nfw]: bit t%64 of word t/64 = tile t's records written
   uint32_t epoch;       // this batch's record tag (1..1023)
+  // One-shard DynamoRIO batches through k_pass1s (kbz_triage_batch_device): k_skip's rule runs
+  // in the kernel's epilogue (p1s_skip_rule), so no k_skip launch follows.  skip == null: k_skip.
+  uint8_t *skip;        // [n] out: row j repeats row j-1's hash (row 0: the context's last hash)
+  uint32_t *fix_flags, *fix_list, *fix_cnt, *bad_list, *bad_cnt;  // bad rows (as k_skip)
+  uint64_t *lastpub;    // [chunks]: tag << 32 | hash of the chunk's last row (look-back)
+  uint32_t tag;         // this batch's look-back tag (never 0)
+  const uint32_t *row0_hp;  // row 0's predecessor hash
+  int pred_saved;           // the saved row (the previous batch's last) is valid ...
+  const uint32_t *pred_ok;  // ... and clean iff *pred_ok
+  const uint8_t *prow;      // the saved row
+  uint32_t *bad0;           // out: row 0 is skipped and differs / has an unknown predecessor
+  uint32_t *err;            // sticky error flags (a look-back that never completes: 512)
 };
 #ifndef KBZ_REC_MAX_WORDS  // a stored tile with more words holding still-virgin bits gets no
 #define KBZ_REC_MAX_WORDS 2  // records (fresh maps, novelty-heavy batches): its claims read rows
@@ -401,6 +413,32 @@ struct Pass1Args {
 // never one, see k_tail).
 constexpr int kRecEpochShift = 54;
 constexpr uint32_t kRecEpochMask = 1023;
+
+// Rows x and y differ on the examined (classified, not ignored) bytes: this thread's part of
+// the map (16 B every `step` bytes from `first`), 8 pairs of loads in flight.
+__device__ __forceinline__ int rows_differ_part(const uint8_t *x, const uint8_t *y,
+                                                const uint8_t *ignore, uint32_t map_size,
+                                                uint32_t first, uint32_t step) {
+  int diff = 0;
+#pragma unroll 8
+  for (uint32_t i = first; i < map_size; i += step) {
+    const uint4 a = *(const uint4 *)(x + i), b = *(const uint4 *)(y + i);
+    const uint64_t a0 = classify8((uint64_t)a.x | ((uint64_t)a.y << 32));
+    const uint64_t a1 = classify8((uint64_t)a.z | ((uint64_t)a.w << 32));
+    const uint64_t b0 = classify8((uint64_t)b.x | ((uint64_t)b.y << 32));
+    const uint64_t b1 = classify8((uint64_t)b.z | ((uint64_t)b.w << 32));
+    uint64_t r0 = ~0ull, r1 = ~0ull;
+    if (ignore) {
+      const uint4 g = *(const uint4 *)(ignore + i);
+      r0 = ~nonzero_bytes8((uint64_t)g.x | ((uint64_t)g.y << 32));
+      r1 = ~nonzero_bytes8((uint64_t)g.z | ((uint64_t)g.w << 32));
+    }
+    diff |= (((a0 ^ b0) & r0) | ((a1 ^ b1) & r1)) != 0;
+  }
+  return diff;
+}
+__device__ void p1s_skip_rule(const Pass1Args &a, uint32_t *sh, int wave, int lane,
+                              uint32_t chunk, uint64_t row0, int nrows);
 
 // ---------------------------------------------------------------------------------------------
 // pass 1: two waves per 64-trace chunk (lane = trace) sharing two 16-KiB LDS tile buffers.
@@ -490,6 +528,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
   constexpr int DL = KBZ_P1S_LEARLY ? D + 1 : D;
   constexpr int SP = DL == D ? D : D * DL;
   const uint32_t nsteps = (ntiles + SP) / SP * SP;
+  uint32_t h32v = 0, neqv = 0;  // this lane's row: hash (L), differs from the previous row (T)
   if (wave == 0) {
     u32x4 R[DL][NLD];
 #pragma unroll
@@ -598,6 +637,11 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
       // (the no-chain ablation stores distinct hashes, so nothing downstream sees repeats)
       const uint32_t h32 = (KBZ_AB_P1S & 32) ? (uint32_t)(row0 + lane) * 2654435761u : h32_final(h);
       a.h32[row0 + lane] = h32;
+      h32v = h32;
+      // the next chunk's row 0 compares with this chunk's last row: publish its hash at once
+      if (MODE == KBZ_MODE_DYNAMORIO && a.skip && lane == nrows - 1 && chunk + 1 < gridDim.x)
+        __hip_atomic_store(&a.lastpub[chunk], ((uint64_t)a.tag << 32) | h32, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
       if (X64 && a.x64) {
         uint64_t xh = rotl64(x0, 1) + rotl64(x1, 7) + rotl64(x2, 12) + rotl64(x3, 18);
         xh = xx_merge(xh, x0);
@@ -609,7 +653,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
       }
       if (row0 + lane == (uint64_t)a.n - 1) {
         a.shard_last[0] = h32;
-        a.shard_last[1] = 1;
+        atomicOr(&a.shard_last[1], 1u);  // (the fused skip rule ORs its bits in meanwhile)
       }
     }
   } else {
@@ -907,7 +951,86 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
     // lane 0 has no predecessor in the wave: its value is a placeholder (k_skip compares a chunk's
     // row 0 with the previous row itself, and only when their hashes are equal)
     if (MODE == KBZ_MODE_DYNAMORIO && valid) a.neq[row0 + lane] = neq != 0;
+    neqv = neq != 0;
   }
+  if (MODE == KBZ_MODE_DYNAMORIO && a.skip) {  // k_skip's rule for this chunk's rows
+    lds_barrier();  // both waves are past their last reads of the tile buffers
+    uint32_t *sh = (uint32_t *)lds;
+    sh[wave * 64 + lane] = wave == 0 ? h32v : neqv;
+    p1s_skip_rule(a, sh, wave, lane, chunk, row0, nrows);
+  }
+}
+
+// k_skip's rule for one chunk of a fused one-shard DynamoRIO batch, in k_pass1s's epilogue: the
+// outputs of k_skip's row blocks, chunk-start blocks and row-0 block for these rows.  sh[0..63]
+// the rows' hashes, sh[64..127] "differs from the previous row" (pass 1's neighbour test; lane
+// 0's is a placeholder).  The chunk's row 0 is compared with its predecessor: the previous
+// chunk's last row, whose hash that workgroup's wave L published in lastpub (a look-back on a
+// lower workgroup: dispatched earlier, and it publishes before any wait of its own), or for
+// chunk 0 the saved row; when the hashes are equal, the two rows themselves (both waves).
+constexpr uint32_t kLookbackSpinMax = 1u << 22;
+__device__ void p1s_skip_rule(const Pass1Args &a, uint32_t *sh, int wave, int lane,
+                              uint32_t chunk, uint64_t row0, int nrows) {
+  if (wave == 1 && lane == 0) {
+    uint32_t hp = 0, known = 1;
+    if (chunk == 0) {
+      hp = *a.row0_hp;
+      known = a.pred_saved && *a.pred_ok != 0;
+    } else {
+      for (uint32_t it = 0;; it++) {
+        const uint64_t pv = __hip_atomic_load(&a.lastpub[chunk - 1], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+        hp = (uint32_t)pv;
+        if ((uint32_t)(pv >> 32) == a.tag) break;
+        if (it == kLookbackSpinMax) {
+          atomicOr(a.err, 512u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    sh[128] = hp;
+    sh[129] = known;
+  }
+  lds_barrier();
+  const bool known = sh[129] != 0;
+  const bool sk0 = sh[0] == sh[128];  // workgroup-uniform
+  bool diff = false;
+  if (sk0 && (chunk > 0 || known)) {  // uniform: the rows themselves, half the map per wave
+    const uint8_t *x = a.traces + row0 * a.stride;
+    const uint8_t *y = chunk > 0 ? x - a.stride : a.prow;
+    const int d = rows_differ_part(x, y, a.ignore, a.map_size, threadIdx.x * 16, blockDim.x * 16);
+    const bool any = __ballot(d) != 0;
+    if (lane == 0) sh[130 + wave] = any;
+    lds_barrier();
+    diff = (sh[130] | sh[131]) != 0;
+  }
+  if (wave != 1) return;
+  const uint64_t j = row0 + lane;
+  bool applied = false, bad = false;
+  if (lane == 0) {
+    a.skip[j] = sk0;
+    if (chunk > 0) {
+      applied = !sk0;
+      if (sk0) a.neq[j] = diff;  // exact now: the chain walks read it
+      bad = sk0 && diff;
+    } else {
+      *a.bad0 = sk0 && (!known || diff);
+    }
+  } else if (lane < nrows) {
+    const bool sk = sh[lane] == sh[lane - 1];
+    a.skip[j] = sk;
+    applied = !sk;
+    bad = sk && sh[64 + lane] != 0;
+  }
+  if (bad) {  // rare (hash collisions): the chunk to the fix list, the row to the chain walks
+    if (atomicExch(&a.fix_flags[chunk], 1u) == 0u) a.fix_list[atomicAdd(a.fix_cnt, 1u)] = chunk;
+    a.bad_list[atomicAdd(a.bad_cnt, 1u)] = (uint32_t)j;
+  }
+  const uint32_t want = (__ballot(bad) ? 2u : 0u) | (__ballot(applied) ? 4u : 0u);
+  if (lane == 0 && (want & ~__hip_atomic_load(&a.shard_last[1], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT)))
+    atomicOr(&a.shard_last[1], want);
 }
 
 // k_pass1w row groups.  X wave xi transforms two groups of wide_rg(xi) consecutive rows (one
@@ -2731,6 +2854,8 @@ struct TailArgs {
   uint32_t *next_last;
   uint32_t *saved_ok;
   uint32_t *flags_w, *fix_list_w, *fix_cnt_w;  // the walks' fix list (DynamoRIO)
+  const uint8_t *copy_src;  // the batch's last row -> the context's saved row (when pass 1 ran
+  uint8_t *copy_dst;        // k_skip's rule, k_skip's copy blocks' role), or null
 };
 #ifndef KBZ_TAIL_INLINE_MAX  // claimed bytes one k_tail wave resolves inline; the rest become
 #define KBZ_TAIL_INLINE_MAX 16  // items, dealt over all of k_fin's waves.  Fresh batches on a warm
@@ -2809,6 +2934,12 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
   KBZ_TAIL_DECL;
   const uint32_t tail_id = ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6);
   (void)tail_id;
+  if (a.copy_src) {  // the batch's last row -> the saved row (the next batch's row-0 predecessor)
+    const uint32_t wg = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const uint32_t step = gridDim.x * gridDim.y * gridDim.z * blockDim.x * 16;
+    for (uint32_t i = (wg * blockDim.x + threadIdx.x) * 16; i < M; i += step)
+      *(uint4 *)(a.copy_dst + i) = *(const uint4 *)(a.copy_src + i);
+  }
   // the next batch's segment ORs start at zero (every segment of this column slice and class)
   if (live)
     for (uint32_t ss = s; ss < kMaxSeg; ss += a.nseg)
@@ -3605,6 +3736,13 @@ struct kbz_ctx {
                                  // [8..10] the last finished batch's [0], [3], [4],
                                  // [12] k_small's workgroup ticket
   uint32_t *shard_last = nullptr;  // [2]
+  // k_pass1s runs k_skip's rule itself for fused one-shard DynamoRIO batches (no k_skip launch;
+  // KBZ_DEBUG_NO_FSKIP=1: k_skip as before)
+  bool fskip_ok = true;
+  uint64_t *lastpub = nullptr;  // [max_chunks] look-back words (tag << 32 | last-row hash)
+  uint32_t skip_tag = 0;
+  const uint8_t *tail_copy_src = nullptr;  // this batch's last row -> saved row, by k_tail
+  uint8_t *tail_copy_dst = nullptr;
   // in-flight shard
   const uint8_t *cur_traces = nullptr;
   size_t cur_n = 0, cur_stride = 0;
@@ -3712,7 +3850,7 @@ void free_ctx(kbz_ctx *c) {
                   c->segprev, c->total,
                   c->items, c->counters, c->shard_last, c->dslot[0], c->dslot[1],
                   c->dslot_oc[0], c->dslot_oc[1], c->dres_hnb, c->dres_h32, c->dres_x64, c->frec,
-                  c->rflags};
+                  c->rflags, c->lastpub};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (int i = 0; i < 2; i++) {
@@ -3950,6 +4088,8 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   if (const char *w = getenv("KBZ_DEBUG_TAIL_INLINE_MAX")) c->inline_max = (uint32_t)std::max(0, atoi(w));
   // tests only: small AFL batches through the general pipeline instead of k_small
   if (const char *w = getenv("KBZ_DEBUG_NO_SMALL")) c->small_ok = atoi(w) == 0;
+  // tests only: fused DynamoRIO batches through k_skip instead of k_pass1s's skip rule
+  if (const char *w = getenv("KBZ_DEBUG_NO_FSKIP")) c->fskip_ok = atoi(w) == 0;
   // tests only: one-shard batches through the staged kernels (k_chain ... k_pack) instead of k_tail
   if (const char *w = getenv("KBZ_DEBUG_STAGED")) c->fused_ok = atoi(w) == 0;
   // tests only: fused DynamoRIO batches without pass-1 claim records (k_tail reads the rows)
@@ -3966,7 +4106,7 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
             !dalloc(&c->tail, kTailFixDone + cdiv(M / 16, 256)) &&
             !dalloc(&c->segprev, kMaxSeg * nc * M) && !dalloc(&c->total, nc * M) &&
             !dalloc(&c->items, c->item_cap) && !dalloc(&c->counters, 16) &&
-            !dalloc(&c->shard_last, 2);
+            !dalloc(&c->shard_last, 2) && !dalloc(&c->lastpub, c->max_chunks);
   if (!ok) {
     std::string e = g_err;
     free_ctx(c);
@@ -3984,6 +4124,7 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   (void)hipMemset(c->last, 0, 2 * sizeof(uint32_t));
   (void)hipMemset(c->counters, 0, 16 * sizeof(uint32_t));
   (void)hipMemset(c->shard_last, 0, 2 * sizeof(uint32_t));
+  (void)hipMemset(c->lastpub, 0, c->max_chunks * sizeof(uint64_t));
   // consumers re-zero these for the next batch (k_total: segor, k_pack: hnb32)
   (void)hipMemset(c->segor, 0, kMaxSeg * nc * M);
   (void)hipMemset(c->segor_alt, 0, kMaxSeg * nc * M);
@@ -4147,7 +4288,7 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
     c->stage = 1;
     return 0;
   }
-  Pass1Args a;
+  Pass1Args a{};
   a.traces = traces;
   a.stride = stride;
   a.n = (uint32_t)n;
@@ -4220,8 +4361,37 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
   const bool stop_on_skip = pev.start && c->mode == KBZ_MODE_DYNAMORIO && KBZ_P1_STOP_ON_NEXT;
   P1Ev pev1 = pev;
   if (stop_on_skip) pev1.stop = nullptr;
+  // a fused DynamoRIO batch through k_pass1s: the kernel runs k_skip's rule itself (its row-0 and
+  // saved-row roles included); the copy of the last row into the context goes to k_tail
+  const bool fsk = fused && c->mode == KBZ_MODE_DYNAMORIO && c->fskip_ok &&
+                   !pass1_is_wide(c->pass1, c->cur_chunks);
+  c->tail_copy_src = nullptr;
+  c->tail_copy_dst = nullptr;
+  if (fsk) {
+    SkipExtra x{};
+    if (fused_link(c, s, &x)) return -1;
+    c->skip_tag = c->skip_tag + 1 ? c->skip_tag + 1 : 1;
+    a.skip = c->skip;
+    a.fix_flags = c->flags;
+    a.fix_list = c->fix_list;
+    a.fix_cnt = c->counters + 3;
+    a.bad_list = c->bad_list;
+    a.bad_cnt = c->counters + 4;
+    a.lastpub = c->lastpub;
+    a.tag = c->skip_tag;
+    a.row0_hp = x.row0_hp;
+    a.pred_saved = x.pred_saved;
+    a.pred_ok = x.pred_ok;
+    a.prow = x.prow;
+    a.bad0 = x.bad0;
+    a.err = c->counters + 2;
+    c->tail_copy_src = x.copy_src;
+    c->tail_copy_dst = x.copy_dst;
+  }
   if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, hashed, s, pev1)) return -1;
-  if (c->mode == KBZ_MODE_DYNAMORIO) {  // the skip rule for rows j >= 1 needs no other shard
+  if (fsk) {
+    fused_link_commit(c);  // pass 1 is queued: this batch's row is the next predecessor
+  } else if (c->mode == KBZ_MODE_DYNAMORIO) {  // the skip rule for rows j >= 1 needs no other shard
     hipEvent_t st0;
     if (stage_begin(c, s, &st0)) return -1;
     const unsigned row_blocks = cdiv(n, 256);
@@ -4319,6 +4489,8 @@ int fused_tail(kbz_ctx *c, uint8_t *hnb_out, hipStream_t s) {
   a.flags_w = c->flags;
   a.fix_list_w = c->fix_list;
   a.fix_cnt_w = c->counters + 3;
+  a.copy_src = c->tail_copy_src;
+  a.copy_dst = c->tail_copy_dst;
   hipEvent_t st0;
   if (stage_begin(c, s, &st0)) return -1;
   const unsigned ncg = cdiv(M / 16, 256);
