@@ -574,7 +574,7 @@ def main_triage(args, pre):
     phase_log = None  # list: per-batch phase timings of the sharded protocol (world > 1)
 
     def step(t, oc):
-        if world == 1:  # one shard: kbz_triage_batch_device (pass 1, k_skip, k_tail, k_fin)
+        if world == 1:  # one shard: kbz_triage_batch_device (pass 1 [+ k_skip], k_tail, k_fin)
             ctx.triage(t, oc, want, out=out)
         else:
             triage_sharded(ctx, t, oc, counts, rank, world, want, device=dev, timings=phase_log)
