@@ -968,7 +968,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
 // chunk's last row, whose hash that workgroup's wave L published in lastpub (a look-back on a
 // lower workgroup: dispatched earlier, and it publishes before any wait of its own), or for
 // chunk 0 the saved row; when the hashes are equal, the two rows themselves (both waves).
-constexpr uint32_t kLookbackSpinMax = 1u << 22;
+constexpr uint32_t kLookbackSpinMax = 1u << 20;  // x ~2 us: a look-back never ends in seconds
 __device__ void p1s_skip_rule(const Pass1Args &a, uint32_t *sh, int wave, int lane,
                               uint32_t chunk, uint64_t row0, int nrows) {
   if (wave == 1 && lane == 0) {
@@ -977,6 +977,10 @@ __device__ void p1s_skip_rule(const Pass1Args &a, uint32_t *sh, int wave, int la
       hp = *a.row0_hp;
       known = a.pred_saved && *a.pred_ok != 0;
     } else {
+      // polls back off to one per ~2 us: on uneven batches (fresh maps) hundreds of workgroups
+      // wait here at once, and tight agent-scope polls take bandwidth from the ones still
+      // streaming
+      uint32_t backoff = 1;
       for (uint32_t it = 0;; it++) {
         const uint64_t pv = __hip_atomic_load(&a.lastpub[chunk - 1], __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
@@ -986,7 +990,8 @@ __device__ void p1s_skip_rule(const Pass1Args &a, uint32_t *sh, int wave, int la
           atomicOr(a.err, 512u);
           break;
         }
-        __builtin_amdgcn_s_sleep(2);
+        for (uint32_t z = 0; z < backoff; z++) __builtin_amdgcn_s_sleep(8);
+        backoff = backoff < 8 ? 2 * backoff : 8;
       }
     }
     sh[128] = hp;
