@@ -537,7 +537,21 @@ def novelty_heavy(args, mode, want, batches, dev, steps=8):
         p1ms, nl = c.time_pass1(False)
         p1 = p1ms / max(1, nl)
         c.sync()
+        # continuity with round 4's figure: steps one at a time (synchronised between steps, the
+        # reset outside the events; round 4 also had stage events on inside them)
+        iso = []
+        for i in range(3):
+            t, oc = batches[(i + 2 + steps) % len(batches)]
+            c.reset_virgin()
+            torch.cuda.synchronize()
+            a.record()
+            c.triage(t, oc, want, out=out)
+            b.record()
+            b.synchronize()
+            iso.append(a.elapsed_time(b))
+        c.sync()
     return {"ms_per_step": round(ms, 4), "pass1_ms": round(p1, 4),
+            "isolated_step_ms": round(sum(iso) / len(iso), 4),
             "stage_ms": {k: round(v, 4) for k, v in stages.items()},
             "claims_per_batch": int(claims),
             "what": f"{steps} never-seen batches back to back, each on all-0xff virgin maps "
