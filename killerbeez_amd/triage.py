@@ -429,6 +429,22 @@ class MultiTriageContext:
         check(lib().kbz_mctx_get_last_hash(self._h, C.byref(out)), "kbz_mctx_get_last_hash")
         return out.value
 
+    @last_hash.setter
+    def last_hash(self, v: int) -> None:
+        """Every worker's context: a worker whose earlier workers hold no rows links its row 0
+        to its own context's last hash."""
+        for w in range(self.workers()):
+            check(lib().kbz_set_last_hash(lib().kbz_mctx_worker(self._h, w), int(v) & 0xFFFFFFFF),
+                  "kbz_set_last_hash")
+
+    def set_ignore(self, ignore) -> None:
+        """DynamoRIO ignore bytes (has_new_bits_with_ignore) on every worker; None clears them."""
+        ig = None if ignore is None else np.ascontiguousarray(ignore, dtype=np.uint8).reshape(
+            self.map_size)
+        for w in range(self.workers()):
+            check(lib().kbz_set_ignore(lib().kbz_mctx_worker(self._h, w),
+                                       None if ig is None else _np_ptr(ig)), "kbz_set_ignore")
+
 
 def triage_modules(ctxs, traces, offsets, outcome=None, stream=None, hashes=False):
     """DynamoRIO per-module coverage (has_new_coverage_per_module,

@@ -75,6 +75,35 @@ def test_sharded_from_c_set_virgin_and_limits(gpu):
         MultiTriageContext(m, 1, 100, devices=[0, 999])
 
 
+@pytest.mark.gpu
+def test_sharded_from_c_ignore_bytes_and_restored_hash(gpu):
+    """DynamoRIO ignore bytes on every worker and a restored last hash (the first row repeats the
+    hash's trace: a skip), two batches, against the oracle with the same ignore bytes."""
+    m = 4096
+    rng = np.random.default_rng(77)
+    ig = (rng.random(m) < 0.3).astype(np.uint8)
+    t, oc = synth.sparse_np(600, m, seed=78, hot_frac=0.05)
+    first = oracle.triage_batch(1, t[:1], oc[:1], want=oracle.WANT_H32)
+    v = np.full((3, m), 0xFF, np.uint8)
+    with MultiTriageContext(m, 1, 256, devices=[0, 0]) as mc:
+        mc.set_ignore(ig)
+        mc.last_hash = int(first["h32"][0])
+        last = int(first["h32"][0])
+        for b in range(2):
+            part = t[300 * b:300 * (b + 1)].copy()
+            if b == 0:
+                part[0] = t[0]  # repeats the restored hash's trace
+            exp = oracle.triage_batch(1, part, oc[300 * b:300 * (b + 1)], virgin=v, ignore=ig,
+                                      last_hash=last, want=oracle.WANT_H32)
+            got = mc.triage_host(part, oc[300 * b:300 * (b + 1)], WANT_H32)
+            np.testing.assert_array_equal(got["hnb"], exp["hnb"])
+            np.testing.assert_array_equal(got["h32"], exp["h32"])
+            np.testing.assert_array_equal(mc.get_virgin(), exp["virgin"])
+            assert mc.last_hash == exp["last_hash"]
+            v, last = exp["virgin"], exp["last_hash"]
+        assert exp is not None
+
+
 def test_mctx_create_fails_loudly_without_a_device():
     """On a host with no GPU the multi-device context refuses to start (no CPU fallback)."""
     import torch
