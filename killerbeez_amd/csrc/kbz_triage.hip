@@ -4800,7 +4800,8 @@ int kbz_sync(kbz_ctx_t *c, void *stream) {
     c->h_err[0] = c->h_err[1] = 0;  // k_pack's host-mapped copy: reported now, not again
     // the inconsistency flags name the site: 2 inline claim (k_scan / k_tail), 8 window item,
     // 16 byte item, 4 / 64 an item never written (k_tail helper / last workgroup), 32 a fix-path
-    // flag never set (k_tail)
+    // flag never set (k_tail), 128 a claim record of another batch, 512 a pass-1 look-back
+    // (k_pass1s's skip rule) that never saw the previous chunk's hash
     char msg[96];
     snprintf(msg, sizeof msg, "inconsistent claim (internal error, flags 0x%x)", cnt[2]);
     return fail(cnt[1] ? "claim list overflow" : msg);
