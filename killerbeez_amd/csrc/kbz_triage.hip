@@ -973,9 +973,9 @@ __device__ void p1s_skip_rule(const Pass1Args &a, uint32_t *sh, int wave, int la
                               uint32_t chunk, uint64_t row0, int nrows) {
   if (wave == 1 && lane == 0) {
     uint32_t hp = 0, known = 1;
-    if (chunk == 0) {
-      hp = *a.row0_hp;
-      known = a.pred_saved && *a.pred_ok != 0;
+    if (chunk == 0) {  // (a shard of the sharded protocol: k_chain links row 0, row0_hp null)
+      hp = a.row0_hp ? *a.row0_hp : ~sh[0];
+      known = a.row0_hp && a.pred_saved && *a.pred_ok != 0;
     } else {
       // polls back off to one per ~2 us: on uneven batches (fresh maps) hundreds of workgroups
       // wait here at once, and tight agent-scope polls take bandwidth from the ones still
@@ -1002,6 +1002,7 @@ __device__ void p1s_skip_rule(const Pass1Args &a, uint32_t *sh, int wave, int la
   const bool sk0 = sh[0] == sh[128];  // workgroup-uniform
   bool diff = false;
   if (sk0 && (chunk > 0 || known)) {  // uniform: the rows themselves, half the map per wave
+    // (chunk 0 of a shard never gets here: its stand-in hash differs from row 0's)
     const uint8_t *x = a.traces + row0 * a.stride;
     const uint8_t *y = chunk > 0 ? x - a.stride : a.prow;
     const int d = rows_differ_part(x, y, a.ignore, a.map_size, threadIdx.x * 16, blockDim.x * 16);
@@ -1014,12 +1015,13 @@ __device__ void p1s_skip_rule(const Pass1Args &a, uint32_t *sh, int wave, int la
   const uint64_t j = row0 + lane;
   bool applied = false, bad = false;
   if (lane == 0) {
-    a.skip[j] = sk0;
     if (chunk > 0) {
+      a.skip[j] = sk0;
       applied = !sk0;
       if (sk0) a.neq[j] = diff;  // exact now: the chain walks read it
       bad = sk0 && diff;
-    } else {
+    } else if (a.row0_hp) {  // one shard: row 0 against the saved row (k_chain's role)
+      a.skip[j] = sk0;
       *a.bad0 = sk0 && (!known || diff);
     }
   } else if (lane < nrows) {
@@ -4368,13 +4370,13 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
   if (stop_on_skip) pev1.stop = nullptr;
   // a fused DynamoRIO batch through k_pass1s: the kernel runs k_skip's rule itself (its row-0 and
   // saved-row roles included); the copy of the last row into the context goes to k_tail
-  const bool fsk = fused && c->mode == KBZ_MODE_DYNAMORIO && c->fskip_ok &&
+  const bool fsk = c->mode == KBZ_MODE_DYNAMORIO && c->fskip_ok &&
                    !pass1_is_wide(c->pass1, c->cur_chunks);
   c->tail_copy_src = nullptr;
   c->tail_copy_dst = nullptr;
-  if (fsk) {
+  if (fsk) {  // (a shard of the sharded protocol: rows j >= 1 only, k_chain links row 0)
     SkipExtra x{};
-    if (fused_link(c, s, &x)) return -1;
+    if (fused && fused_link(c, s, &x)) return -1;
     c->skip_tag = c->skip_tag + 1 ? c->skip_tag + 1 : 1;
     a.skip = c->skip;
     a.fix_flags = c->flags;
@@ -4395,7 +4397,7 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
   }
   if (pass1_dispatch(c, a, c->cur_chunks, a.x64 != nullptr, hashed, s, pev1)) return -1;
   if (fsk) {
-    fused_link_commit(c);  // pass 1 is queued: this batch's row is the next predecessor
+    if (fused) fused_link_commit(c);  // pass 1 is queued: this batch's row is the next predecessor
   } else if (c->mode == KBZ_MODE_DYNAMORIO) {  // the skip rule for rows j >= 1 needs no other shard
     hipEvent_t st0;
     if (stage_begin(c, s, &st0)) return -1;
