@@ -157,7 +157,7 @@ def max_over_ranks(x, world, dev):
 def finish(world):
     import torch.distributed as dist
 
-    if world > 1:
+    if dist.is_initialized():  # (world 1: the sharded-protocol variant's one-rank group)
         dist.destroy_process_group()
 
 
@@ -559,6 +559,59 @@ def novelty_heavy(args, mode, want, batches, dev, steps=8):
                     "stage_ms from one extra untimed step with stage events"}
 
 
+def sharded_world1(args, ctx, batches, counts, want, dev, timed, fused_ms):
+    """The N > 1 step at N = 1: the same fresh batches through dist.triage_sharded with
+    force_collective on a one-rank RCCL communicator (both all-gathers run), so the protocol's
+    cost over the fused one-shard step is measured on a one-GPU box; phase times from HIP
+    events around each phase."""
+    import torch
+    import torch.distributed as dist
+
+    from killerbeez_amd.dist import timing_summary, triage_sharded
+
+    try:
+        if not dist.is_initialized():
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}",
+                                    rank=0, world_size=1, device_id=dev)
+        log = []
+        el_box = {}
+
+        def sharded_step(t, oc):
+            triage_sharded(ctx, t, oc, counts[:1], 0, 1, want, device=dev, timings=log,
+                           force_collective=True)
+
+        # warm the communicator and the staged kernels, then the timed steps (phase events on)
+        for t, oc in batches[:2]:
+            sharded_step(t, oc)
+        torch.cuda.synchronize()
+        log.clear()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            sharded_step(*batches[i % len(batches)])
+        torch.cuda.synchronize()
+        el_box["s"] = time.perf_counter() - t0
+        phases = timing_summary(log)
+        # the same steps without phase events (the events add their own gaps)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            triage_sharded(ctx, *batches[i % len(batches)], counts[:1], 0, 1, want, device=dev,
+                           force_collective=True)
+        torch.cuda.synchronize()
+        ms = 1e3 * (time.perf_counter() - t0) / args.steps
+        return {"ms_per_step": round(ms, 4), "fused_ms_per_step": round(fused_ms, 4),
+                "extra_us_per_step": round(1e3 * (ms - fused_ms), 1),
+                "ms_per_step_with_phase_events": round(1e3 * el_box["s"] / args.steps, 4),
+                "phase_ms": {k: round(v, 4) for k, v in phases.items()},
+                "backend": dist.get_backend(),
+                "what": "the fresh batches again through triage_sharded(force_collective=True) on "
+                        "a one-rank RCCL group (the N>1 step's kernels and both all-gathers), "
+                        "virgin carried; fused_ms_per_step = the headline's step"}
+    except Exception as e:  # noqa: BLE001
+        return {"error": f"{type(e).__name__}: {e}"[:300]}
+
+
 def main_triage(args, pre):
     import torch
 
@@ -664,6 +717,9 @@ def main_triage(args, pre):
         if world == 1:
             variants["afl_all_crash_simplify"] = crash_variant(args, pool, barrier_sync, dev)
             variants["novelty_heavy"] = novelty_heavy(args, mode, want, fresh, dev)
+            if not dense:
+                variants["sharded_protocol_world1"] = sharded_world1(
+                    args, ctx, fresh, counts, want, dev, timed, 1e3 * elapsed / args.steps)
     del pool, fresh
     traffic = pre["traffic"]
     if traffic is None:
@@ -996,6 +1052,30 @@ def table_insert_rate(dev, n=1 << 20, batches=8):
 
 # ---- plugin per-exec latency -------------------------------------------------------------------
 
+def plugin_loop_c(name, t, oc, M, pool_rows=2048):
+    """tools/plugin_loop (built by build()) in a child process, one run per batch size."""
+    import subprocess
+    import tempfile
+
+    from killerbeez_amd import build
+
+    if not os.path.exists(build.PLUGIN_LOOP):
+        raise SystemExit(f"{build.PLUGIN_LOOP} is missing: run build() first")
+    dr = name == "dynamorio"
+    out = {"by_batch": {}}
+    with tempfile.TemporaryDirectory() as d:
+        pf, of = os.path.join(d, "pool.bin"), os.path.join(d, "oc.bin")
+        t[:pool_rows].tofile(pf)
+        oc[:pool_rows].astype(np.int8).tofile(of)
+        for bs, execs in ((1, 512 if dr else 4096), (16, 4096), (256, 8192), (4096, 16384)):
+            r = subprocess.run([build.PLUGIN_LOOP, name, pf, of, str(M), str(pool_rows),
+                                str(execs), str(bs)], capture_output=True, text=True, timeout=300)
+            if r.returncode:
+                raise SystemExit(f"plugin_loop failed: {r.stderr[-500:]}")
+            out["by_batch"].update(json.loads(r.stdout)["by_batch"])
+    return out
+
+
 def main_plugin(args, pre=None):
     """Per-exec latency of the instrumentation plugin (libkbz_plugin.so, include/kbz_plugin.h)
     driven like fuzzer/main.c:370-418: every exec's raw trace is recorded, its novelty queried.
@@ -1008,9 +1088,14 @@ def main_plugin(args, pre=None):
 
     from killerbeez_amd import build, synth
 
-    torch.cuda.set_device(0)
     M = args.map_size
     name = "dynamorio" if args.mode == "dynamorio" else "afl"
+    t, oc = synth.sparse_np(8192, M, seed=args.seed)
+    if name == "dynamorio":
+        oc[:] = 0
+    # first, before this process touches the GPU: the loop from C (tools/plugin_loop.c)
+    c_loop = plugin_loop_c(name, t, oc, M)
+    torch.cuda.set_device(0)
     L = C.CDLL(build.PLUGIN_LIB)
     create = getattr(L, f"kbz_{name}_gpu_create")
     create.restype, create.argtypes = C.c_void_p, [C.c_char_p, C.c_char_p]
@@ -1020,9 +1105,6 @@ def main_plugin(args, pre=None):
     result.restype, result.argtypes = C.c_int, [C.c_void_p, C.c_long]
     cleanup = getattr(L, f"kbz_{name}_gpu_cleanup")
     cleanup.argtypes = [C.c_void_p]
-    t, oc = synth.sparse_np(8192, M, seed=args.seed)
-    if name == "dynamorio":
-        oc[:] = 0
 
     def per_exec(pool):
         """us per exec at each batch size; traces taken round-robin from the first `pool` rows"""
@@ -1053,17 +1135,25 @@ def main_plugin(args, pre=None):
     # cycled, the record copies from cache as it does from the target's just-written shm map
     per = per_exec(8192)
     per_hot = per_exec(16)
+    by_c = {b: v["plugin_us"] for b, v in c_loop["by_batch"].items()}
     res = {"metric": "per-exec triage latency through the instrumentation plugin",
-           "value": per["1"], "unit": "us/exec", "n_gpus": 1, "steps": 1, "warmup": 1,
+           "value": by_c["1"], "unit": "us/exec", "n_gpus": 1, "steps": 1, "warmup": 1,
            "higher_is_better": False, "vs_baseline": None, "dtype": "u8",
            "data": "synthetic config-2 traces in host memory",
-           "config": {"workload": f"plugin {name}_gpu: record + result per exec, batch sizes "
-                                  "1/16/256/4096", "map_size": M, "mode": args.mode},
-           "us_per_exec_by_batch": per,
-           "us_per_exec_by_batch_hot_source": per_hot,
-           "source_note": "us_per_exec_by_batch: each record copies a trace from a 512 MiB pool "
-                          "(DRAM-cold); _hot_source: 16 traces cycled (cache-resident, as the "
-                          "target's freshly written shm map is)"}
+           "config": {"workload": f"plugin {name}_gpu: record + result per exec from C in the "
+                                  "fuzz loop's shape, batch sizes 1/16/256/4096",
+                      "map_size": M, "mode": args.mode},
+           "us_per_exec_by_batch": by_c,
+           "c_loop": c_loop,
+           "c_loop_note": "tools/plugin_loop.c: per exec memset(map) + the target's write of its "
+                          "trace into a SysV shm map + record; every B execs result() for the B "
+                          "tickets.  us_per_exec_by_batch = plugin_us = loop - the same loop "
+                          "without the two plugin calls (base_us, timed after each loop)",
+           "python_us_per_exec_by_batch": per,
+           "python_us_per_exec_by_batch_hot_source": per_hot,
+           "python_note": "the same calls through ctypes from Python (two foreign calls per exec "
+                          "included): each record copies a trace from a 512 MiB pool "
+                          "(DRAM-cold); _hot_source: 16 traces cycled"}
     if not args.no_cpu:
         cb = cpu_baseline(torch.from_numpy(t), torch.from_numpy(oc),
                           1 if name == "dynamorio" else 0, min(args.cpu_seconds, 5.0))

@@ -169,9 +169,15 @@ int kbz_triage_batch_host(kbz_ctx_t *ctx, const uint8_t *traces, size_t n, size_
  *   kbz_ring_submit: triages the slot's first n rows (outcome array used if have_outcome);
  *     returns at once.  hnb_out/h32_out/x64_out are host buffers (NULL = not wanted), filled
  *     when the slot is acquired again or at kbz_ring_flush.
+ *   kbz_ring_commit (optional): rows [0, n_ready) of the acquired slot are written (and, if the
+ *     producer used streaming stores, fenced): their host-to-device copy starts now, while the
+ *     producer keeps filling the slot, and kbz_ring_submit copies only the rest.  Without it a
+ *     batch's whole copy waits for the submit.  A slot with committed rows is always triaged
+ *     from device memory (batches of <= 64 uncommitted rows are read from the pinned slot).
  *   kbz_ring_flush: waits for every submitted batch, delivers results, reports device errors.
  * Do not interleave with kbz_triage_batch_host on the same context (they share the slots). */
 int kbz_ring_acquire(kbz_ctx_t *ctx, uint8_t **rows, int8_t **outcome, size_t *cap);
+int kbz_ring_commit(kbz_ctx_t *ctx, size_t n_ready);
 int kbz_ring_submit(kbz_ctx_t *ctx, size_t n, int have_outcome, uint8_t *hnb_out,
                     uint32_t *h32_out, uint64_t *x64_out, int want);
 int kbz_ring_flush(kbz_ctx_t *ctx);

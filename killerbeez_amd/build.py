@@ -32,6 +32,9 @@ HIP_SOURCES = [os.path.join(CSRC, "kbz_triage.hip"), os.path.join(CSRC, "kbz_set
 HIP_HEADERS = [os.path.join(CSRC, "kbz_device.h"), os.path.join(INC, "kbz_triage.h")]
 PLUGIN_SOURCES = [os.path.join(CSRC, "kbz_plugin.c")]
 PLUGIN_HEADERS = [os.path.join(INC, "kbz_plugin.h"), os.path.join(INC, "kbz_triage.h")]
+# bench harness (not product): the plugins driven from C in the fuzz loop's shape
+PLUGIN_LOOP = os.path.join(ROOT, "tools", "plugin_loop")
+PLUGIN_LOOP_SRC = os.path.join(ROOT, "tools", "plugin_loop.c")
 
 
 class BuildError(RuntimeError):
@@ -72,12 +75,13 @@ def hipcc() -> str:
     return "hipcc"
 
 
-def _hip_cmd(out, defines) -> list:
-    # kbz_build_flags() reports the -D flags of a variant build (the product passes none)
-    tag = " ".join(defines)
+def _hip_cmd(out, defines, csrc=CSRC, tag_extra="") -> list:
+    # kbz_build_flags() reports the -D flags (and patch) of a variant build (the product: "")
+    tag = " ".join(defines) + tag_extra
+    sources = [os.path.join(csrc, os.path.basename(f)) for f in HIP_SOURCES]
     return [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-            "-Wall", "-Wno-unused-function", "-I", INC, "-I", CSRC, *defines,
-            f"-DKBZ_BUILD_FLAGS_STR=\"{tag}\"", *HIP_SOURCES, "-ldl", "-o", out + ".tmp"]
+            "-Wall", "-Wno-unused-function", "-I", INC, "-I", csrc, *defines,
+            f"-DKBZ_BUILD_FLAGS_STR=\"{tag}\"", *sources, "-ldl", "-o", out + ".tmp"]
 
 
 def build_hip(force: bool = False, verbose: bool = False) -> str:
@@ -91,9 +95,12 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     return HIP_LIB
 
 
-def build_variant(name: str, defines, verbose: bool = False) -> str:
+def build_variant(name: str, defines, verbose: bool = False, patch: str | None = None) -> str:
     """Experiment build: build_variants/<name>/libkbz_hip.so with extra -D flags.  Load it
-    with KBZ_HIP_LIB=<path>; it never replaces the product library."""
+    with KBZ_HIP_LIB=<path>; it never replaces the product library.  `patch` (a unified diff
+    against csrc/, e.g. tools/ab_p1s.patch: timing-only ablations with wrong results) is applied
+    to a copy of the sources in build_variants/<name>/csrc -- such code never enters the
+    product tree."""
     defines = list(defines)
     bad = [d for d in defines if not d.startswith("-D") or '"' in d]
     if bad or not name or os.sep in name:
@@ -101,8 +108,18 @@ def build_variant(name: str, defines, verbose: bool = False) -> str:
     out_dir = os.path.join(VARIANTS, name)
     os.makedirs(out_dir, exist_ok=True)
     out = os.path.join(out_dir, "libkbz_hip.so")
-    cmd = _hip_cmd(out, defines)
-    deps = HIP_SOURCES + HIP_HEADERS
+    csrc, extra = CSRC, ""
+    if patch:
+        import shutil
+
+        csrc = os.path.join(out_dir, "csrc")
+        shutil.rmtree(csrc, ignore_errors=True)
+        shutil.copytree(CSRC, csrc, ignore=shutil.ignore_patterns("*.so*", "__pycache__"))
+        with open(patch) as f:
+            subprocess.check_call(["patch", "-s", "-p1", "-d", csrc], stdin=f)
+        extra = f" patch={os.path.basename(patch)}"
+    cmd = _hip_cmd(out, defines, csrc, extra)
+    deps = HIP_SOURCES + HIP_HEADERS + ([patch] if patch else [])
     if not _up_to_date(out, cmd, deps):
         _run(out, cmd, deps, verbose)
     return out
@@ -121,14 +138,29 @@ def build_plugin(force: bool = False, verbose: bool = False) -> str:
     return PLUGIN_LIB
 
 
+def build_plugin_loop(force: bool = False, verbose: bool = False) -> str:
+    if not os.path.exists(PLUGIN_LOOP_SRC):
+        return ""
+    cmd = ["gcc", "-O2", "-Wall", "-std=gnu11", "-I", INC, PLUGIN_LOOP_SRC, "-L", PKG,
+           "-lkbz_plugin", "-Wl,-rpath,$ORIGIN/../killerbeez_amd", "-o", PLUGIN_LOOP + ".tmp"]
+    deps = [PLUGIN_LOOP_SRC, os.path.join(INC, "kbz_plugin.h"), PLUGIN_LIB + ".stamp"]
+    if force or not _up_to_date(PLUGIN_LOOP, cmd, deps):
+        _run(PLUGIN_LOOP, cmd, deps, verbose)
+    return PLUGIN_LOOP
+
+
 def build_all(force: bool = False, verbose: bool = False) -> None:
     build_hip(force, verbose)
     build_plugin(force, verbose)
+    build_plugin_loop(force, verbose)
 
 
 if __name__ == "__main__":
     args = sys.argv[1:]
     if args[:1] == ["--variant"] and len(args) >= 2:
-        print(build_variant(args[1], args[2:], verbose=True))
+        rest, patch = args[2:], None
+        if rest[:1] == ["--patch"] and len(rest) >= 2:
+            patch, rest = os.path.abspath(rest[1]), rest[2:]
+        print(build_variant(args[1], rest, verbose=True, patch=patch))
     else:
         build_all(force="--force" in args, verbose=True)

@@ -133,6 +133,8 @@ typedef struct kbz_plugin {
    * setup_shm_and_pick_fuzzer_id(state, 1) resets the virgin maps (see dr_first_enable) */
   int dr_enabled;
   unsigned long dump_failures;  /* dump_map_dir / get_module_info bookkeeping that failed */
+  int early_copy;          /* start large windows' host-to-device copy while recording (default
+                            * 1; KBZ_PLUGIN_EARLY_COPY=0 for A/B runs) */
 } kbz_plugin_t;
 
 static size_t nmaps(const kbz_plugin_t *p) { return p->mode == KBZ_MODE_DYNAMORIO ? 1 : 3; }
@@ -464,6 +466,8 @@ static kbz_plugin_t *plugin_alloc(int mode, size_t map_size, size_t max_batch) {
   p->last_ticket = -1;
   p->last_fuzz_result = KBZ_PLUGIN_FUZZ_ERROR;
   p->restored_status = 0;
+  const char *ec = getenv("KBZ_PLUGIN_EARLY_COPY");
+  p->early_copy = !ec || atoi(ec) != 0;
   p->virgin = (uint8_t *)malloc(3 * map_size);
   p->r_hnb = (uint8_t *)malloc(max_batch);
   if (!p->virgin || !p->r_hnb) {
@@ -895,6 +899,14 @@ static long plugin_record(kbz_plugin_t *p, const uint8_t *trace, int fuzz_result
   p->q_outcome[p->q_n] = (int8_t)fuzz_result;
   p->last_ticket = p->q_base + (long)p->q_n++;
   p->last_fuzz_result = fuzz_result;
+  /* every 64 execs past the first 128 (a window that will not fit the pinned-read path of
+   * <= 64 rows): the rows recorded so far start their copy to the GPU now, overlapped with the
+   * execs still to come, instead of all at the result query.  The copy is only started early;
+   * if it cannot be, the flush copies those rows itself. */
+  if (p->early_copy && !p->per_module && p->q_n >= 128 && (p->q_n & 63) == 0) {
+    slot_copies_done();
+    (void)kbz_ring_commit(p->ctx, p->q_n);
+  }
   return p->last_ticket;
 }
 

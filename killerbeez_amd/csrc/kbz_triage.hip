@@ -346,10 +346,6 @@ __device__ __forceinline__ uint32_t byte_xform(uint32_t b, int xf) {
 #ifndef KBZ_P1S_ORGATE  // k_pass1s: column ORs only for words where some row holds a virgin bit
 #define KBZ_P1S_ORGATE 1
 #endif
-#ifndef KBZ_AB_P1S  // timing-only ablations of k_pass1s (wrong results; variant builds only):
-#define KBZ_AB_P1S 0  // 1 no column OR, 2 no neighbour test, 4 no classify, 8 no mix, 16 wave T
-#endif                // skips the word loop, 32 wave L skips the chain, 64 no segment-OR
-                      // atomics, 128 no chunk_or stores
 #ifndef KBZ_WIDE_PEEL  // k_pass1w transform waves: steady steps without bounds tests
 #define KBZ_WIDE_PEEL 1
 #endif
@@ -401,6 +397,7 @@ struct Pass1Args {
   const uint8_t *prow;      // the saved row
   uint32_t *bad0;           // out: row 0 is skipped and differs / has an unknown predecessor
   uint32_t *err;            // sticky error flags (a look-back that never completes: 512)
+  uint32_t spin_max;        // look-back polls before that (tests force 0: the fallback path)
 };
 #ifndef KBZ_REC_MAX_WORDS  // a stored tile with more words holding still-virgin bits gets no
 #define KBZ_REC_MAX_WORDS 2  // records (fresh maps, novelty-heavy batches): its claims read rows
@@ -602,7 +599,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         for (int u = 0; u < DL; u++) {
           const uint32_t s = g + u;
           load_half(R[u], s + DL);
-          if (!(KBZ_AB_P1S & 32) && s >= 1 && s <= ntiles) chain_tile(s - 1, (s - 1) & 1);
+          if (s >= 1 && s <= ntiles) chain_tile(s - 1, (s - 1) & 1);
           KBZ_STAMP(0);
           vmcnt_wait<(DL - 1) * NLD>();
           KBZ_STAMP(1);
@@ -619,7 +616,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
 #pragma unroll
         for (int u = 0; u < D; u++) {
           const uint32_t s = g + u;
-          if (!(KBZ_AB_P1S & 32) && s >= 1 && s <= ntiles) chain_tile(s - 1, (s - 1) & 1);
+          if (s >= 1 && s <= ntiles) chain_tile(s - 1, (s - 1) & 1);
           KBZ_STAMP(0);
           vmcnt_wait<(D - 1) * NLD>();
           KBZ_STAMP(1);
@@ -635,7 +632,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
     drain_asm_loads(R);
     if (valid) {
       // (the no-chain ablation stores distinct hashes, so nothing downstream sees repeats)
-      const uint32_t h32 = (KBZ_AB_P1S & 32) ? (uint32_t)(row0 + lane) * 2654435761u : h32_final(h);
+      const uint32_t h32 = h32_final(h);
       a.h32[row0 + lane] = h32;
       h32v = h32;
       // the next chunk's row 0 compares with this chunk's last row: publish its hash at once
@@ -775,7 +772,7 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         // uniform index, written back mixed for wave L.
         constexpr int G = KBZ_P1S_GROUP > 0 ? KBZ_P1S_GROUP : 1;  // (the branch is dead at 0)
         uint32_t nzm = 0;
-        if (!(KBZ_AB_P1S & 16)) {
+        {
           uint4 vv[SLOTS];
 #pragma unroll
           for (int q = 0; q < SLOTS; q++) vv[q] = row[q ^ sw];
@@ -851,10 +848,10 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         for (int e = 0; e < 2; e++) {
           const int wi = 2 * q + e;
           const uint64_t x = ld_u64(v, e);
-          if (!(KBZ_AB_P1S & 16) && __ballot(x != 0)) {
-            const uint64_t tw = (KBZ_AB_P1S & 4) ? x : xform8(x, xf);
+          if (__ballot(x != 0)) {
+            const uint64_t tw = xform8(x, xf);
             // what wave L chains next step (with ignore bytes the mix sees the kept bytes only)
-            const uint64_t out = (TMIX && !(KBZ_AB_P1S & 8)) ? h32_mix_mad(tw & (IGN ? ig[wi] : ~0ull)) : tw;
+            const uint64_t out = TMIX ? h32_mix_mad(tw & (IGN ? ig[wi] : ~0ull)) : tw;
             if (e) { v.z = (uint32_t)out; v.w = (uint32_t)(out >> 32); }
             else { v.x = (uint32_t)out; v.y = (uint32_t)(out >> 32); }
             dirty = true;
@@ -870,16 +867,16 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
                       __builtin_amdgcn_readlane((uint32_t)vlane[k], wi);
                   const uint64_t c = (valid && cls == k) ? (tw & vw) : 0;
                   if (__ballot(c != 0)) {
-                    const uint64_t r = (KBZ_AB_P1S & 1) ? c : wave_or64(c);
+                    const uint64_t r = wave_or64(c);
                     orw[k] = (lane == wi) ? r : orw[k];
                   }
                 } else {
-                  const uint64_t r = (KBZ_AB_P1S & 1) ? tw : wave_or64((valid && cls == k) ? tw : 0);
+                  const uint64_t r = wave_or64((valid && cls == k) ? tw : 0);
                   orw[k] = (lane == wi) ? r : orw[k];
                 }
               }
             }
-            if (MODE == KBZ_MODE_DYNAMORIO && !(KBZ_AB_P1S & 2)) {
+            if (MODE == KBZ_MODE_DYNAMORIO) {
               const uint64_t rel = IGN ? ~nonzero_bytes8(ig[wi]) : ~0ull;
               neq |= (tw ^ from_prev_lane(tw)) & rel;
             }
@@ -905,13 +902,13 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
         const uint64_t m = orw[k] & vlane[k];
         if (__ballot(lane < TW / 8 && m != 0)) {
           tfl[k] |= 1ull << (s & 63);
-          if (!(KBZ_AB_P1S & 128) && lane < TW / 8)
+          if (lane < TW / 8)
             *(uint64_t *)(a.chunk_or + (size_t)chunk * NC * a.map_size + off) = m;
           if (REC && a.frec && tile_records(s, b, m)) rfl |= 1ull << (s & 63);
         }
         // segment aggregate, restricted to still-virgin bits like chunk_or (its consumers only
         // use it under & V: k_scan's segment test and V' = V & ~total): almost never an atomic
-        if (!(KBZ_AB_P1S & 64) && lane < TW / 8 && m)
+        if (lane < TW / 8 && m)
           atomicOr((unsigned long long *)(a.segor + (size_t)seg * NC * a.map_size + off),
                    (unsigned long long)m);
         if ((s & 63) == 63 || s + 1 == ntiles) {
@@ -968,7 +965,19 @@ __global__ __launch_bounds__(128, 2) void k_pass1s(Pass1Args a) {
 // chunk's last row, whose hash that workgroup's wave L published in lastpub (a look-back on a
 // lower workgroup: dispatched earlier, and it publishes before any wait of its own), or for
 // chunk 0 the saved row; when the hashes are equal, the two rows themselves (both waves).
-constexpr uint32_t kLookbackSpinMax = 1u << 20;  // x ~2 us: a look-back never ends in seconds
+// hash32 of one DynamoRIO row as pass 1 chains it (hash32_with_ignore over the classified map,
+// winafl_hash.h:80-112; without ignore bytes the plain hash32, afl_progs/hash.h:36-65): one lane,
+// direct loads
+__device__ uint32_t row_hash32_dr(const uint8_t *row, const uint8_t *ignore, uint32_t map_size) {
+  uint64_t h = (uint64_t)(kHashConst ^ map_size);
+  for (uint32_t w = 0; w < map_size / 8; w++) {
+    uint64_t k = classify8(*(const uint64_t *)(row + 8 * (size_t)w));
+    if (ignore) k &= *(const uint64_t *)(ignore + 8 * (size_t)w);
+    h = h32_step(h, h32_mix(k));
+  }
+  return h32_final(h);
+}
+// look-back polls (Pass1Args::spin_max, default 2^20 x ~2 us: a look-back never ends in seconds)
 __device__ void p1s_skip_rule(const Pass1Args &a, uint32_t *sh, int wave, int lane,
                               uint32_t chunk, uint64_t row0, int nrows) {
   if (wave == 1 && lane == 0) {
@@ -986,8 +995,12 @@ __device__ void p1s_skip_rule(const Pass1Args &a, uint32_t *sh, int wave, int la
                                               __HIP_MEMORY_SCOPE_AGENT);
         hp = (uint32_t)pv;
         if ((uint32_t)(pv >> 32) == a.tag) break;
-        if (it == kLookbackSpinMax) {
+        if (it >= a.spin_max) {
+          // the lower workgroup never published: the stall is reported (512), and the
+          // predecessor's hash is recomputed from its row here (8 K dependent steps: a path
+          // that should never run), so the skip rule below stays exact
           atomicOr(a.err, 512u);
+          hp = row_hash32_dr(a.traces + (row0 - 1) * a.stride, a.ignore, a.map_size);
           break;
         }
         for (uint32_t z = 0; z < backoff; z++) __builtin_amdgcn_s_sleep(8);
@@ -3746,6 +3759,7 @@ struct kbz_ctx {
   // k_pass1s runs k_skip's rule itself for fused one-shard DynamoRIO batches (no k_skip launch;
   // KBZ_DEBUG_NO_FSKIP=1: k_skip as before)
   bool fskip_ok = true;
+  uint32_t spin_max = 1u << 20;  // kLookbackSpinMax; KBZ_DEBUG_LOOKBACK_SPIN overrides (tests)
   uint64_t *lastpub = nullptr;  // [max_chunks] look-back words (tag << 32 | last-row hash)
   uint32_t skip_tag = 0;
   const uint8_t *tail_copy_src = nullptr;  // this batch's last row -> saved row, by k_tail
@@ -3772,6 +3786,12 @@ struct kbz_ctx {
   uint64_t *dres_x64 = nullptr;
   size_t slot_rows = 0;
   hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_used[2] = {nullptr, nullptr};
+  // kbz_reset_virgin on a caller's stream: the next batch's stream waits for ev_reset (the host
+  // paths run on work_stream, which nothing else orders after the caller's stream); ev_prior
+  // orders the fill after batches still queued on work_stream
+  hipEvent_t ev_reset = nullptr, ev_prior = nullptr;
+  hipStream_t reset_stream = nullptr;
+  bool reset_pending = false;
   // pinned ingest ring (kbz_ring_*): per slot, device + pinned results and the pending
   // delivery of the batch last submitted from it
   struct RingSlot {
@@ -3784,6 +3804,7 @@ struct kbz_ctx {
     uint32_t *m_h32 = nullptr;
     uint64_t *m_x64 = nullptr;
     size_t n = 0;
+    size_t copied = 0;  // rows [0, copied) already queued for the device slot (kbz_ring_commit)
     bool pending = false;
     uint8_t *hnb_out = nullptr;
     uint32_t *h32_out = nullptr;
@@ -3876,6 +3897,8 @@ void free_ctx(kbz_ctx *c) {
     (void)hipEventDestroy(e.second);
   }
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+  if (c->ev_reset) (void)hipEventDestroy(c->ev_reset);
+  if (c->ev_prior) (void)hipEventDestroy(c->ev_prior);
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->work_stream) (void)hipStreamDestroy(c->work_stream);
@@ -4097,6 +4120,7 @@ kbz_ctx_t *kbz_ctx_create(size_t map_size, int mode, size_t max_batch) {
   if (const char *w = getenv("KBZ_DEBUG_NO_SMALL")) c->small_ok = atoi(w) == 0;
   // tests only: fused DynamoRIO batches through k_skip instead of k_pass1s's skip rule
   if (const char *w = getenv("KBZ_DEBUG_NO_FSKIP")) c->fskip_ok = atoi(w) == 0;
+  if (const char *w = getenv("KBZ_DEBUG_LOOKBACK_SPIN")) c->spin_max = (uint32_t)strtoul(w, 0, 0);
   // tests only: one-shard batches through the staged kernels (k_chain ... k_pack) instead of k_tail
   if (const char *w = getenv("KBZ_DEBUG_STAGED")) c->fused_ok = atoi(w) == 0;
   // tests only: fused DynamoRIO batches without pass-1 claim records (k_tail reads the rows)
@@ -4184,8 +4208,22 @@ int kbz_set_virgin(kbz_ctx_t *c, const uint8_t *in) {
 int kbz_reset_virgin(kbz_ctx_t *c, void *stream) {
   if (!c) return fail("null argument");
   DevGuard g(c->device);
+  const hipStream_t s = (hipStream_t)stream;
+  if (!c->ev_reset) {
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_prior, hipEventDisableTiming));
+  }
+  // a host batch or ring submit still queued on work_stream writes the buffer filled here (its
+  // V' is the next batch's V): the fill comes after it
+  if (c->work_stream && c->work_stream != s) {
+    HIP_TRY(hipEventRecord(c->ev_prior, c->work_stream));
+    HIP_TRY(hipStreamWaitEvent(s, c->ev_prior, 0));
+  }
   // the buffer the next enqueued batch reads (vcur flips when a batch is enqueued)
-  HIP_TRY(hipMemsetAsync(c->V[c->vcur], 0xff, 3 * c->M, (hipStream_t)stream));
+  HIP_TRY(hipMemsetAsync(c->V[c->vcur], 0xff, 3 * c->M, s));
+  HIP_TRY(hipEventRecord(c->ev_reset, s));
+  c->reset_stream = s;
+  c->reset_pending = true;  // the next batch's stream waits for the fill (shard_begin_impl)
   c->saved_valid = false;  // as kbz_set_virgin: the saved row's bits may not be in the new maps
   return 0;
 }
@@ -4253,6 +4291,13 @@ uint8_t *kbz_virgin_device(kbz_ctx_t *c) { return c ? c->V[c->vcur] : nullptr; }
 namespace {
 int fused_link(kbz_ctx *c, hipStream_t s, SkipExtra *x);
 void fused_link_commit(kbz_ctx *c);
+// kbz_reset_virgin's fill, queued on another stream, comes before the next batch on stream s
+int wait_reset(kbz_ctx *c, hipStream_t s) {
+  if (!c->reset_pending) return 0;
+  if (c->reset_stream != s) HIP_TRY(hipStreamWaitEvent(s, c->ev_reset, 0));
+  c->reset_pending = false;
+  return 0;
+}
 // kbz_shard_begin; with `fused` (a one-shard batch of kbz_triage_batch_device) k_skip takes
 // k_chain's row-0 and saved-row roles (the fused tail).
 int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
@@ -4263,6 +4308,7 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
   if (n && check_rows(traces, stride, c->M)) return -1;
   DevGuard g(c->device);
   hipStream_t s = (hipStream_t)stream;
+  if (wait_reset(c, s)) return -1;
   if (c->stage != 0) {
     // the previous batch was abandoned between stages (e.g. a collective failed): re-arm what
     // its later kernels would have reset -- the per-batch counters, fix-list flags, the shard's
@@ -4392,6 +4438,7 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
     a.prow = x.prow;
     a.bad0 = x.bad0;
     a.err = c->counters + 2;
+    a.spin_max = c->spin_max;
     c->tail_copy_src = x.copy_src;
     c->tail_copy_dst = x.copy_dst;
   }
@@ -4724,6 +4771,7 @@ int kbz_triage_batch_device(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_
     if (check_rows(traces, stride, c->M)) return -1;
     if (n > c->max_batch) return fail("n exceeds max_batch");
     DevGuard g(c->device);
+    if (wait_reset(c, (hipStream_t)stream)) return -1;
     const int vn = c->vcur ^ 1;
     SmallArgs a{traces, stride, (uint32_t)n, (uint32_t)c->M, outcome, c->V[c->vcur], c->V[vn],
                 c->hnb32, hnb_out, c->counters + 12, c->counters + 8};
@@ -4796,7 +4844,6 @@ int kbz_sync(kbz_ctx_t *c, void *stream) {
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   uint32_t cnt[4];
   HIP_TRY(hipMemcpy(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost));
-  if (KBZ_AB_P1S) cnt[1] = cnt[2] = 0;  // timing-only ablation builds: results are wrong anyway
   if (cnt[1] || cnt[2]) {  // sticky until reported here
     HIP_TRY(hipMemset(c->counters + 1, 0, 2 * sizeof(uint32_t)));
     c->h_err[0] = c->h_err[1] = 0;  // k_pack's host-mapped copy: reported now, not again
@@ -4955,6 +5002,7 @@ int kbz_ring_acquire(kbz_ctx_t *c, uint8_t **rows, int8_t **outcome, size_t *cap
   // next acquire starts clean instead of finding a slot it never received still held
   if (ring_errors(c)) return -1;
   c->ring_acquired = sl;
+  c->ring[sl].copied = 0;
   *rows = c->pin[sl];
   if (outcome) *outcome = c->pin_oc[sl];
   if (cap) *cap = c->slot_rows;
@@ -4976,14 +5024,15 @@ int kbz_ring_submit(kbz_ctx_t *c, size_t n, int have_outcome, uint8_t *hnb_out,
   auto &r = c->ring[sl];
   const size_t M = c->M;
   const bool x64 = (want & KBZ_WANT_X64) && x64_out;
-  if (n <= kZeroCopyRows) {
+  if (n <= kZeroCopyRows && r.copied == 0) {
     if (kbz_triage_batch_device(c, r.m_rows, n, M, have_outcome ? r.m_oc : nullptr, r.m_hnb,
                                 h32_out ? r.m_h32 : nullptr, x64 ? r.m_x64 : nullptr, want,
                                 c->work_stream))
       return -1;
   } else {
-    HIP_TRY(hipMemcpyAsync(c->dslot[sl], c->pin[sl], n * M, hipMemcpyHostToDevice,
-                           c->copy_stream));
+    if (n > r.copied)  // the rows kbz_ring_commit has not queued yet
+      HIP_TRY(hipMemcpyAsync(c->dslot[sl] + r.copied * M, c->pin[sl] + r.copied * M,
+                             (n - r.copied) * M, hipMemcpyHostToDevice, c->copy_stream));
     if (have_outcome)
       HIP_TRY(hipMemcpyAsync(c->dslot_oc[sl], c->pin_oc[sl], n, hipMemcpyHostToDevice,
                              c->copy_stream));
@@ -5009,6 +5058,24 @@ int kbz_ring_submit(kbz_ctx_t *c, size_t n, int have_outcome, uint8_t *hnb_out,
   r.pending = true;
   c->ring_acquired = -1;
   c->ring_next = sl ^ 1;
+  return 0;
+}
+
+// Rows [0, n_ready) of the acquired slot are final: their H2D copy starts now, on the copy
+// stream, while the producer keeps filling the slot (the submit then copies only the rest).
+int kbz_ring_commit(kbz_ctx_t *c, size_t n_ready) {
+  if (!c) return fail("null ctx");
+  const int sl = c->ring_acquired;
+  if (sl < 0) return fail("kbz_ring_commit: no slot acquired");
+  if (n_ready > c->slot_rows) return fail("kbz_ring_commit: n_ready exceeds the slot capacity");
+  auto &r = c->ring[sl];
+  if (n_ready <= r.copied) return 0;
+  DevGuard g(c->device);
+  const size_t M = c->M;
+  // the slot's previous batch is done (kbz_ring_acquire waited for it): its device rows are free
+  HIP_TRY(hipMemcpyAsync(c->dslot[sl] + r.copied * M, c->pin[sl] + r.copied * M,
+                         (n_ready - r.copied) * M, hipMemcpyHostToDevice, c->copy_stream));
+  r.copied = n_ready;
   return 0;
 }
 

@@ -34,6 +34,22 @@ def _stream_handle(stream):
     return C.c_void_p(stream.cuda_stream)
 
 
+def _host_batch(traces, outcome, map_size):
+    """A host batch as the C side reads it: uint8 rows of exactly map_size bytes (stride =
+    map_size) and, if given, one int8 outcome per row -- checked here, since a narrower array or
+    a short outcome would make the C copies read past the caller's buffers."""
+    t = np.ascontiguousarray(traces, dtype=np.uint8)
+    if t.ndim != 2 or t.shape[1] != map_size:
+        raise ValueError(f"traces must be 2-D [n, {map_size}], got shape {t.shape}")
+    oc = None
+    if outcome is not None:
+        oc = np.ascontiguousarray(outcome, dtype=np.int8)
+        if oc.ndim != 1 or oc.shape[0] != t.shape[0]:
+            raise ValueError(f"outcome must hold one entry per trace ({t.shape[0]}), got shape "
+                             f"{oc.shape}")
+    return t, oc
+
+
 def nclass(mode: int) -> int:
     return 1 if mode == MODE_DYNAMORIO else 3
 
@@ -188,9 +204,8 @@ class TriageContext:
 
     def triage_host(self, traces: np.ndarray, outcome=None, want: int = WANT_H32):
         """Host-memory batch (numpy uint8 [n, map_size]); streamed through pinned slots."""
-        t = np.ascontiguousarray(traces, dtype=np.uint8)
+        t, oc = _host_batch(traces, outcome, self.map_size)
         n = t.shape[0]
-        oc = None if outcome is None else np.ascontiguousarray(outcome, dtype=np.int8)
         hnb = np.zeros(n, np.uint8)
         h32 = np.zeros(n, np.uint32) if want & WANT_H32 else None
         x64 = np.zeros(n, np.uint64) if want & WANT_X64 else None
@@ -222,6 +237,10 @@ class TriageContext:
         acquired again or at ring_flush (keep them alive until then)."""
         check(lib().kbz_ring_submit(self._h, n, int(bool(have_outcome)), _np_ptr(hnb_out),
                                     _np_ptr(h32_out), _np_ptr(x64_out), want), "kbz_ring_submit")
+
+    def ring_commit(self, n_ready):
+        """Rows [0, n_ready) of the acquired slot are written: start their copy to the GPU."""
+        check(lib().kbz_ring_commit(self._h, n_ready), "kbz_ring_commit")
 
     def ring_flush(self):
         check(lib().kbz_ring_flush(self._h), "kbz_ring_flush")
@@ -404,11 +423,10 @@ class MultiTriageContext:
         return lib().kbz_mctx_workers(self._h)
 
     def triage_host(self, traces: np.ndarray, outcome=None, want: int = WANT_H32):
-        t = np.ascontiguousarray(traces, dtype=np.uint8)
+        t, oc = _host_batch(traces, outcome, self.map_size)
         n = t.shape[0]
         hnb = np.zeros(n, np.uint8)
         h32 = np.zeros(n, np.uint32)
-        oc = None if outcome is None else np.ascontiguousarray(outcome, dtype=np.int8)
         check(lib().kbz_triage_batch_devices(self._h, _np_ptr(t) if n else None, n, self.map_size,
                                              None if oc is None else _np_ptr(oc), _np_ptr(hnb),
                                              _np_ptr(h32), want), "kbz_triage_batch_devices")

@@ -3,7 +3,8 @@
 # under rocprofv3 --kernel-trace --stats itself, so the traced pass-1 dispatches are the ones
 # its JSON line timed (scripts/ktrace_summary.py compares them).  Every GPU step has its own
 # time limit; the first failure ends the call.
-#   TAG=name TESTS="tests/test_rccl.py ..." LEGS="name|args;..." DIRECT="name|args;..."
+#   TAG=name TESTS="tests/test_rccl.py ..." KEXPR="pytest -k expression" LEGS="name|args;..."
+#   DIRECT="name|args;..."
 cd "${GRAFT_REPO_ROOT}" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r05}; mkdir -p $O
@@ -13,7 +14,7 @@ HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 if [ -n "$TESTS" ]; then
   step "pytest $TESTS"
-  timeout -k 10 ${TEST_LIMIT:-600} python -u -m pytest $TESTS -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1 || { tail -30 $O/pytest_gpu.txt; exit 1; }
+  timeout -k 10 ${TEST_LIMIT:-600} python -u -m pytest $TESTS ${KEXPR:+-k "$KEXPR"} -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1 || { tail -30 $O/pytest_gpu.txt; exit 1; }
   tail -1 $O/pytest_gpu.txt
 fi
 if [ -n "$SMOKE" ]; then

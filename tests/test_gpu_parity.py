@@ -383,10 +383,14 @@ def test_sharded_protocol_on_gpu(gpu, mode, counts):
         assert batch == 0 or 0 < (hnb > 0).sum() < n  # later batches still find something
 
 
+@pytest.mark.parametrize("commit", [False, True], ids=["submit-copies", "early-commits"])
 @pytest.mark.parametrize("mode", MODES)
-def test_ingest_ring(gpu, mode):
+def test_ingest_ring(gpu, mode, commit):
     """kbz_ring_*: the producer writes rows into pinned slots, batches are queued back to back
-    (results delivered on re-acquire / flush) and equal one sequential pass over all traces."""
+    (results delivered on re-acquire / flush) and equal one sequential pass over all traces.
+    early-commits: rows are written in pieces and kbz_ring_commit starts each piece's copy
+    (17-row pieces: a small batch with committed rows goes through device memory; a commit of
+    every row, of none, and a repeated commit)."""
     m, sizes = 4096, [300, 17, 0, 256, 1, 300]
     ctx = TriageContext(m, mode, 300)
     t, oc = synth.sparse_np(sum(sizes), m, seed=77, hot_frac=0.05)
@@ -398,7 +402,16 @@ def test_ingest_ring(gpu, mode):
     for i, n in enumerate(sizes):
         rows, ocs = ctx.ring_acquire()
         assert rows.shape[0] >= n and rows.shape[1] == m
-        rows[:n] = t[lo:lo + n]
+        if commit:
+            ctx.ring_commit(0)
+            for a in range(0, n, 17):
+                b = min(n, a + 17)
+                rows[a:b] = t[lo + a:lo + b]
+                if b < n or i % 2:  # odd batches commit every row, even ones leave a tail
+                    ctx.ring_commit(b)
+                    ctx.ring_commit(b)
+        else:
+            rows[:n] = t[lo:lo + n]
         ocs[:n] = oc[lo:lo + n]
         hnb = np.full(n, 0xEE, np.uint8)
         h32 = np.zeros(n, np.uint32)
@@ -623,6 +636,43 @@ def test_dynamorio_restored_hash_unknown_predecessor(gpu):
     ctx.close()
 
 
+@pytest.mark.parametrize("with_ignore", [False, True])
+def test_lookback_timeout_recomputes_predecessor_hash(gpu, monkeypatch, with_ignore):
+    """k_pass1s's fused skip rule with a look-back that gives up at once
+    (KBZ_DEBUG_LOOKBACK_SPIN=0): a chunk whose lower neighbour has not published yet recomputes
+    that neighbour's last-row hash from the row (hash32 / hash32_with_ignore of the classified
+    map) instead of using a stale word.  Results stay exact; the stall is reported as flag 0x200
+    when it happened."""
+    import torch
+
+    from killerbeez_amd._lib import KbzError
+
+    monkeypatch.setenv("KBZ_DEBUG_LOOKBACK_SPIN", "0")
+    m = 4096
+    rng = np.random.default_rng(4411)
+    t, oc = synth.sparse_np(N_AT_SCALE, m, seed=4412, hot_frac=0.05)
+    ign = None
+    if with_ignore:
+        ign = np.where(rng.random(m) < 0.4, 0, rng.integers(1, 256, size=m)).astype(np.uint8)
+        _collide(t, 64 * 9, np.nonzero(ign == 0)[0], rng)  # a collision at a chunk start
+    for c in range(1, 513, 2):
+        t[64 * c] = t[64 * c - 1]           # repeats at chunk starts: row 0's rule decides
+    exp = oracle.triage_batch(MODE_DYNAMORIO, t, oc, ignore=ign, want=oracle.WANT_H32)
+    with TriageContext(m, MODE_DYNAMORIO, N_AT_SCALE) as ctx:
+        if ign is not None:
+            ctx.set_ignore(ign)
+        out = ctx.triage(torch.from_numpy(t).cuda(), torch.from_numpy(oc).cuda(), WANT_H32)
+        torch.cuda.synchronize()
+        try:
+            ctx.sync()
+        except KbzError as e:
+            assert "0x200" in str(e), e
+        np.testing.assert_array_equal(out["hnb"].cpu().numpy(), exp["hnb"])
+        np.testing.assert_array_equal(out["h32"].cpu().numpy().view(np.uint32), exp["h32"])
+        np.testing.assert_array_equal(ctx.get_virgin(), exp["virgin"])
+        assert ctx.last_hash == exp["last_hash"]
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_at_scale_x64_partial_chunk(gpu, mode):
     m = 256
@@ -758,6 +808,51 @@ def test_reset_virgin_is_stream_ordered(gpu, mode):
         if mode == MODE_DYNAMORIO:
             assert ctx.last_hash == exp_b["last_hash"]
             assert exp_b["hnb"][0] == 0 and exp_b["hnb"][1] > 0
+
+
+@pytest.mark.parametrize("path", ["host", "ring"])
+@pytest.mark.parametrize("mode", MODES)
+def test_reset_virgin_then_host_batch(gpu, mode, path):
+    """kbz_reset_virgin on the caller's stream (torch's current stream, held busy by a long
+    kernel so the fill lands late), then a host batch (kbz_triage_batch_host) or a ring submit:
+    both run on the context's own non-blocking stream, which must wait for the fill.  And the
+    other order: a ring batch still queued when the reset is issued is not overwritten by it."""
+    import torch
+
+    m = 4096
+    t, oc = synth.sparse_np(300, m, seed=2087 + mode, hot_frac=0.05)
+    a, b = t[:150].copy(), t[150:].copy()
+    fresh = np.full((3, m), 0xFF, np.uint8)
+    exp_a = oracle.triage_batch(mode, a, oc[:150], virgin=fresh, want=oracle.WANT_H32)
+    exp_b = oracle.triage_batch(mode, b, oc[150:], virgin=fresh, last_hash=exp_a["last_hash"],
+                                want=oracle.WANT_H32)
+    with TriageContext(m, mode, 150) as ctx:
+        if path == "host":
+            ra = ctx.triage_host(a, oc[:150], WANT_H32)
+        else:
+            rows, roc = ctx.ring_acquire()
+            rows[:150] = a
+            roc[:150] = oc[:150]
+            ra = {"hnb": np.zeros(150, np.uint8)}
+            ctx.ring_submit(150, True, ra["hnb"])  # still queued when the reset is issued
+        torch.cuda._sleep(50_000_000)  # ~20 ms of GPU time ahead of the fill on this stream
+        ctx.reset_virgin()
+        if path == "host":
+            rb = ctx.triage_host(b, oc[150:], WANT_H32)
+        else:
+            rows, roc = ctx.ring_acquire()
+            rows[:150] = b
+            roc[:150] = oc[150:]
+            rb = {"hnb": np.zeros(150, np.uint8)}
+            ctx.ring_submit(150, True, rb["hnb"])
+            ctx.ring_flush()
+        torch.cuda.synchronize()
+        ctx.sync()
+        np.testing.assert_array_equal(ra["hnb"], exp_a["hnb"])
+        np.testing.assert_array_equal(rb["hnb"], exp_b["hnb"])
+        np.testing.assert_array_equal(ctx.get_virgin(), exp_b["virgin"])
+        if mode == MODE_DYNAMORIO:
+            assert ctx.last_hash == exp_b["last_hash"]
 
 
 def test_claim_overflow_is_reported_once(gpu, monkeypatch):

@@ -199,6 +199,31 @@ def test_deferred_and_batched(gpu, name, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name,mode", MODES)
+def test_deferred_windows_with_early_copies(gpu, name, mode):
+    """Windows of more than 128 recorded execs start copying every 64 execs while recording
+    (kbz_ring_commit); windows of 200, 256 (one full max_batch: flushed by the next record) and
+    130 execs, with repeats across the commit points, equal the sequential per-exec results."""
+    n = 200 + 256 + 1 + 130
+    t, oc = synth.sparse_np(n, M, seed=23, hot_frac=0.05, outcome_p=(0.8, 0.1, 0.1))
+    t[128] = t[127]
+    t[192:200] = t[191]
+    t[200 + 64] = t[200 + 63]
+    exp = _expected(mode, t, oc)
+    p = P.Plugin(name, f'{{"map_size": {M}, "max_batch": 256}}')
+    got, lo = [], 0
+    for w in (200, 257, 130):
+        tickets = [p.record(t[j], int(oc[j])) for j in range(lo, lo + w)]
+        got += [p.result(k) for k in tickets]
+        lo += w
+    np.testing.assert_array_equal(np.array(got, np.uint8), exp["hnb"])
+    got_maps = P.state_maps(p.get_state(), M)
+    np.testing.assert_array_equal(got_maps["virgin_bits"], exp["virgin"][0])
+    if name == "dynamorio_gpu":
+        assert got_maps["last_shm_hash"] == exp["last_hash"]
+
+
+@pytest.mark.gpu
 def test_dynamorio_ignore_file(gpu, tmp_path):
     rng = np.random.default_rng(4)
     ign = np.where(rng.random(M) < 0.4, 0, rng.integers(1, 256, M)).astype(np.uint8)
