@@ -999,10 +999,48 @@ def main_stream(args, pre=None):
            "pcie_frac": round(gbps / pcie["value"], 4),
            "xxh64_table_insert": ins,
            "unique_crash_hang_keys": table.size(), "new_keys_reported": int(n_new)}
+    ctx.close()
+    if world == 1:
+        res["multi_device_host_batch"] = multi_device_host_batch(args, host, hoc, pcie)
     if rank == 0:
         print(json.dumps(res), flush=True)
-    ctx.close()
     finish(world)
+
+
+def multi_device_host_batch(args, host, hoc, pcie, reps=3):
+    """The one-process sharded path from C (kbz_triage_batch_devices): a pageable host batch
+    split over workers, each staged on its own host thread through pinned slots, then the
+    sharded protocol over the workers' devices.  Workers: every visible GPU, or 1 and 2 workers
+    sharing cuda:0 on a one-GPU box (one PCIe link).  Reported against the pinned H2D peak of
+    the same run (per link)."""
+    import torch
+
+    from killerbeez_amd.triage import MODES, WANT_H32, MultiTriageContext
+
+    ngpu = torch.cuda.device_count()
+    layouts = [list(range(ngpu))] if ngpu > 1 else [[0], [0, 0]]
+    out = {}
+    M, n = args.map_size, host.shape[0]
+    for devs in layouts:
+        try:
+            with MultiTriageContext(M, MODES[args.mode], -(-n // len(devs)), devices=devs) as mc:
+                mc.triage_host(host, hoc, WANT_H32)  # warm: staging slots, contexts
+                best = float("inf")
+                for _ in range(reps):
+                    t0 = time.perf_counter()
+                    mc.triage_host(host, hoc, WANT_H32)
+                    best = min(best, time.perf_counter() - t0)
+                gbps = n * M / best / 1e9
+                links = len(set(devs))
+                out[f"workers{len(devs)}_gpus{links}"] = {
+                    "traces_per_s": round(n / best, 1), "GBps": round(gbps, 2),
+                    "frac_of_pinned_h2d_peak": round(gbps / (links * pcie["value"]), 4),
+                    "peer_pairs": mc.peer_pairs()}
+        except Exception as e:  # noqa: BLE001
+            out[f"workers{len(devs)}"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    out["what"] = (f"{n} traces x {M} B from pageable host memory per call (best of {reps}), "
+                   "host to results, virgin carried; peak = pinned H2D per GPU link")
+    return out
 
 
 def pcie_h2d_peak(dev, mib=256, reps=8):

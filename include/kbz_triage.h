@@ -224,6 +224,24 @@ size_t kbz_shard_aggregate_bytes(kbz_ctx_t *ctx);
 int kbz_shard_finish(kbz_ctx_t *ctx, const uint8_t *prefix, const uint8_t *total,
                      uint8_t *hnb_out, void *stream);
 
+/* The same protocol with fewer launches per step (round 6; killerbeez_amd/dist.py uses it):
+ *   kbz_shard_exchange_row: the shard's last row and hash pair in ONE launch: d_out[0, M) = the
+ *     last row (untouched for an empty shard), d_out[M, M + 8) = the pair, as kbz_shard_last_row
+ *     + kbz_shard_last_hash write them (d_out 16-B aligned: a slot of the all-gather buffer).
+ *   kbz_shard_reduce_into: in place of kbz_shard_reduce + kbz_shard_aggregate: the fix path and
+ *     the shard's OR aggregate written straight into d_aggregate (nclass*map_size bytes, device,
+ *     8-B aligned; e.g. this rank's slot of the all-gather buffer), the segment ORs kept.
+ *   kbz_shard_finish_gathered: in place of kbz_or_prefix_total + kbz_shard_finish: the
+ *     all-gathered aggregates d_gathered[world][nclass*map_size] (16-B aligned) give the prefix
+ *     of ranks < rank and the batch total inside the fused tail (k_tail + k_fin, as a one-shard
+ *     batch runs it).  A single shard passes its own aggregate with rank 0, world 1.
+ * Order: begin, [DynamoRIO: exchange_row, all-gather, link], reduce_into, all-gather,
+ * finish_gathered. */
+int kbz_shard_exchange_row(kbz_ctx_t *ctx, uint8_t *d_out, void *stream);
+int kbz_shard_reduce_into(kbz_ctx_t *ctx, uint8_t *d_aggregate, void *stream);
+int kbz_shard_finish_gathered(kbz_ctx_t *ctx, const uint8_t *d_gathered, size_t rank,
+                              size_t world, uint8_t *hnb_out, void *stream);
+
 /* out[i] = OR of in[r*bytes + i] for r in [r_lo, r_hi).  Device, stream-ordered. */
 int kbz_or_reduce(uint8_t *out, const uint8_t *in, size_t r_lo, size_t r_hi, size_t bytes,
                   void *stream);
@@ -284,7 +302,17 @@ int kbz_merge_and_fill_devices(uint8_t *out, size_t n, size_t state_bytes, kbz_m
  * uint8[n], or NULL) and h32_out (host uint32[n], or NULL; DynamoRIO always hashes) get the
  * results of one sequential pass over the whole batch -- the reference's per-exec
  * has_new_bits / has_new_coverage -- and every worker's virgin maps and last hash become that
- * pass's.  XXH64 is not offered here (KBZ_WANT_X64 fails).  Synchronous. */
+ * pass's.  XXH64 is not offered here (KBZ_WANT_X64 fails).  Synchronous.
+ * Host batches are staged per worker on the worker's own host thread through two pinned slots
+ * (the host copy of one slot overlaps the DMA of the other), all workers at once.
+ * kbz_mctx_create enables peer access between every pair of the workers' distinct devices
+ * (hipDeviceEnablePeerAccess) so the exchanges' peer copies run over xGMI;
+ * kbz_mctx_peer_pairs returns how many ordered device pairs have it (0 on one GPU).
+ * kbz_triage_batch_devices_resident: the same protocol on a batch already on the devices --
+ * worker w's n[w] rows at traces[w] (device memory of devices[w], rows `stride` apart, stride
+ * >= map_size and a multiple of 16), the batch being worker 0's rows, then worker 1's, ...;
+ * outcome (array of W device int8 pointers, or NULL), hnb_out / h32_out (arrays of W device
+ * pointers on the workers' devices; the array or an entry may be NULL).  Synchronous. */
 typedef struct kbz_mctx kbz_mctx_t;
 kbz_mctx_t *kbz_mctx_create(size_t map_size, int mode, size_t max_batch, const int *devices,
                             size_t ndev);
@@ -294,6 +322,11 @@ kbz_ctx_t *kbz_mctx_worker(kbz_mctx_t *m, size_t w);  /* its context (ignore byt
 int kbz_triage_batch_devices(kbz_mctx_t *m, const uint8_t *traces, size_t n, size_t stride,
                              const int8_t *outcome, uint8_t *hnb_out, uint32_t *h32_out,
                              int want);
+int kbz_triage_batch_devices_resident(kbz_mctx_t *m, const uint8_t *const *traces,
+                                      const size_t *n, size_t stride,
+                                      const int8_t *const *outcome, uint8_t *const *hnb_out,
+                                      uint32_t *const *h32_out, int want);
+int kbz_mctx_peer_pairs(kbz_mctx_t *m);
 /* Worker 0's virgin maps / last hash (every worker holds the same); set_virgin sets all. */
 int kbz_mctx_get_virgin(kbz_mctx_t *m, uint8_t *host_out);
 int kbz_mctx_set_virgin(kbz_mctx_t *m, const uint8_t *host_in);

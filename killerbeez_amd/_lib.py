@@ -48,6 +48,9 @@ SIGNATURES = [
     ("kbz_shard_aggregate", _i, [_vp, _vp, _vp]),
     ("kbz_shard_aggregate_bytes", _sz, [_vp]),
     ("kbz_shard_finish", _i, [_vp, _vp, _vp, _vp, _vp]),
+    ("kbz_shard_exchange_row", _i, [_vp, _vp, _vp]),
+    ("kbz_shard_reduce_into", _i, [_vp, _vp, _vp]),
+    ("kbz_shard_finish_gathered", _i, [_vp, _vp, _sz, _sz, _vp, _vp]),
     ("kbz_or_reduce", _i, [_vp, _vp, _sz, _sz, _sz, _vp]),
     ("kbz_or_prefix_total", _i, [_vp, _vp, _vp, _sz, _sz, _sz, _vp]),
     ("kbz_merge_and_device", _i, [_vp, _vp, _sz, _sz, _vp]),
@@ -60,6 +63,8 @@ SIGNATURES = [
     ("kbz_mctx_workers", _i, [_vp]),
     ("kbz_mctx_worker", _vp, [_vp, _sz]),
     ("kbz_triage_batch_devices", _i, [_vp, _vp, _sz, _sz, _vp, _vp, _vp, _i]),
+    ("kbz_triage_batch_devices_resident", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp, _i]),
+    ("kbz_mctx_peer_pairs", _i, [_vp]),
     ("kbz_mctx_get_virgin", _i, [_vp, _vp]),
     ("kbz_mctx_set_virgin", _i, [_vp, _vp]),
     ("kbz_mctx_get_last_hash", _i, [_vp, C.POINTER(_u32)]),

@@ -112,6 +112,28 @@ struct DevScope {  // restore the calling thread's device
   }
 };
 
+// Peer access between every pair of distinct devices in devs (both directions), so peer copies
+// (hipMemcpyPeerAsync) go GPU to GPU over xGMI instead of staging through host memory.  Pairs
+// the platform cannot connect are left alone (their copies still work, staged by the runtime).
+// Returns the number of ordered pairs with peer access enabled.
+int enable_peers(const std::vector<int> &devs) {
+  std::vector<int> d = devs;
+  std::sort(d.begin(), d.end());
+  d.erase(std::unique(d.begin(), d.end()), d.end());
+  int pairs = 0;
+  for (int a : d)
+    for (int b : d) {
+      if (a == b) continue;
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) continue;
+      if (hipSetDevice(a) != hipSuccess) continue;
+      const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+      if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) pairs++;
+      (void)hipGetLastError();  // an "already enabled" is not an error of a later call
+    }
+  return pairs;
+}
+
 // RCCL exchange: one ncclAllGather of every worker's fold over comms from ncclCommInitAll (one
 // rank per distinct GPU), then a local AND of the gathered rows on every device.  Every stream
 // is synchronised before the communicators are destroyed (no collective or AND still queued on
@@ -193,6 +215,7 @@ extern "C" int kbz_merge_and_fill_devices(uint8_t *out, size_t n, size_t state_b
   }
   if (used_out) *used_out = use_rccl ? KBZ_EXCHANGE_RCCL : KBZ_EXCHANGE_COPY;
   if (state_bytes == 0) return 0;
+  if (!use_rccl) (void)enable_peers(devs);  // the copy exchange's peer copies over xGMI
   if (n == 0) {
     memset(out, 0xff, state_bytes);
     return 0;
@@ -278,16 +301,22 @@ extern "C" int kbz_merge_and_fill_devices(uint8_t *out, size_t n, size_t state_b
 // triage") driven by one host thread over W workers, each a kbz_ctx on its device with its own
 // stream: contiguous shards of a host batch, the DynamoRIO link rows and the OR aggregates
 // exchanged by peer copies (device-local copies for workers sharing a GPU) into a gather buffer
-// on every worker, one kbz_or_prefix_total per worker.  Cross-stream order by events only: no
-// host sync until the results are copied back.
+// on every worker (each worker's own aggregate written into its slot by kbz_shard_reduce_into),
+// prefix and total taken inside kbz_shard_finish_gathered.  Cross-stream order by events only:
+// no host sync until the results are copied back.
 struct kbz_mctx {
   size_t M = 0, max_batch = 0, W = 0, ab = 0;  // ab = aggregate bytes per worker
   int mode = 0;
+  int peer_pairs = 0;  // ordered pairs of the workers' distinct devices with peer access on
+  size_t stage_rows = 0;  // host batches: rows per pinned staging slot (2 slots per worker)
   std::vector<int> dev;
+  std::vector<uint8_t *> pin[2];   // per worker: pinned staging slots (host batches)
+  std::vector<int8_t *> pin_oc;    // per worker: pinned outcome staging (max_batch)
+  std::vector<hipEvent_t> ev_slot[2];
   std::vector<kbz_ctx_t *> ctx;
   std::vector<hipStream_t> s;
   std::vector<hipEvent_t> ev_link, ev_agg;
-  std::vector<uint8_t *> traces, hnb, mine, gather, agg_mine, agg_all, prefix, total;
+  std::vector<uint8_t *> traces, hnb, mine, gather, agg_all;
   std::vector<int8_t *> oc;
   std::vector<uint32_t *> h32;
 };
@@ -297,13 +326,17 @@ void mctx_free(kbz_mctx *m) {
   for (size_t w = 0; w < m->W; w++) {
     if (w < m->dev.size()) (void)hipSetDevice(m->dev[w]);
     if (w < m->s.size() && m->s[w]) (void)hipStreamSynchronize(m->s[w]);
-    for (auto *v : {&m->traces, &m->hnb, &m->mine, &m->gather, &m->agg_mine, &m->agg_all,
-                    &m->prefix, &m->total})
+    for (auto *v : {&m->traces, &m->hnb, &m->mine, &m->gather, &m->agg_all})
       if (w < v->size() && (*v)[w]) (void)hipFree((*v)[w]);
     if (w < m->oc.size() && m->oc[w]) (void)hipFree(m->oc[w]);
     if (w < m->h32.size() && m->h32[w]) (void)hipFree(m->h32[w]);
     if (w < m->ev_link.size() && m->ev_link[w]) (void)hipEventDestroy(m->ev_link[w]);
     if (w < m->ev_agg.size() && m->ev_agg[w]) (void)hipEventDestroy(m->ev_agg[w]);
+    for (int i = 0; i < 2; i++) {
+      if (w < m->pin[i].size() && m->pin[i][w]) (void)hipHostFree(m->pin[i][w]);
+      if (w < m->ev_slot[i].size() && m->ev_slot[i][w]) (void)hipEventDestroy(m->ev_slot[i][w]);
+    }
+    if (w < m->pin_oc.size() && m->pin_oc[w]) (void)hipHostFree(m->pin_oc[w]);
     if (w < m->ctx.size() && m->ctx[w]) kbz_ctx_destroy(m->ctx[w]);
     if (w < m->s.size() && m->s[w]) (void)hipStreamDestroy(m->s[w]);
   }
@@ -340,15 +373,20 @@ extern "C" kbz_mctx_t *kbz_mctx_create(size_t map_size, int mode, size_t max_bat
   m->W = ndev;
   m->dev.assign(devices, devices + ndev);
   const size_t W = ndev, row = map_size + 16;  // gathered link rows: [row | hash pair | pad]
-  for (auto *v : {&m->traces, &m->hnb, &m->mine, &m->gather, &m->agg_mine, &m->agg_all,
-                  &m->prefix, &m->total})
-    v->assign(W, nullptr);
+  for (auto *v : {&m->traces, &m->hnb, &m->mine, &m->gather, &m->agg_all}) v->assign(W, nullptr);
   m->oc.assign(W, nullptr);
   m->h32.assign(W, nullptr);
   m->ctx.assign(W, nullptr);
   m->s.assign(W, nullptr);
   m->ev_link.assign(W, nullptr);
   m->ev_agg.assign(W, nullptr);
+  for (int i = 0; i < 2; i++) {
+    m->pin[i].assign(W, nullptr);
+    m->ev_slot[i].assign(W, nullptr);
+  }
+  m->pin_oc.assign(W, nullptr);
+  // staging slots of up to 32 MiB (at least one row, at most a shard)
+  m->stage_rows = std::max<size_t>(1, std::min(max_batch, (size_t)(32u << 20) / map_size));
   auto bad = [&](const char *what) {
     std::string msg = std::string("kbz_mctx_create: ") + what;
     mctx_free(m);
@@ -369,13 +407,17 @@ extern "C" kbz_mctx_t *kbz_mctx_create(size_t map_size, int mode, size_t max_bat
         hipMalloc((void **)&m->hnb[w], max_batch + 16) != hipSuccess ||
         hipMalloc((void **)&m->mine[w], row) != hipSuccess ||
         hipMalloc((void **)&m->gather[w], W * row) != hipSuccess ||
-        hipMalloc((void **)&m->agg_mine[w], m->ab) != hipSuccess ||
-        hipMalloc((void **)&m->agg_all[w], W * m->ab) != hipSuccess ||
-        hipMalloc((void **)&m->prefix[w], m->ab) != hipSuccess ||
-        hipMalloc((void **)&m->total[w], m->ab) != hipSuccess)
+        hipMalloc((void **)&m->agg_all[w], W * m->ab) != hipSuccess)
       return bad("out of device memory");
     if (hipMemset(m->mine[w], 0, row) != hipSuccess) return bad("hipMemset");
+    for (int i = 0; i < 2; i++)
+      if (hipHostMalloc((void **)&m->pin[i][w], m->stage_rows * map_size, 0) != hipSuccess ||
+          hipEventCreateWithFlags(&m->ev_slot[i][w], hipEventDisableTiming) != hipSuccess)
+        return bad("out of pinned host memory");
+    if (hipHostMalloc((void **)&m->pin_oc[w], max_batch + 16, 0) != hipSuccess)
+      return bad("out of pinned host memory");
   }
+  m->peer_pairs = enable_peers(m->dev);
   return m;
 }
 
@@ -390,40 +432,70 @@ extern "C" kbz_ctx_t *kbz_mctx_worker(kbz_mctx_t *m, size_t w) {
   return (m && w < m->W) ? m->ctx[w] : nullptr;
 }
 
-extern "C" int kbz_triage_batch_devices(kbz_mctx_t *m, const uint8_t *traces, size_t n,
-                                        size_t stride, const int8_t *outcome, uint8_t *hnb_out,
-                                        uint32_t *h32_out, int want) {
-  if (!m) return fail_multi("null mctx");
-  if (n && (!traces || stride < m->M)) return fail_multi("bad traces / stride");
-  if (want & KBZ_WANT_X64) return fail_multi("kbz_triage_batch_devices: XXH64 is not gathered");
+extern "C" int kbz_mctx_peer_pairs(kbz_mctx_t *m) { return m ? m->peer_pairs : -1; }
+
+namespace {
+// Rows [r0, r1) of a host shard (stride apart) into a pinned slot, split over up to `nt` threads
+// (one thread's copy out of pageable memory runs well below the PCIe rate).
+void fill_rows(uint8_t *dst, const uint8_t *src, size_t rows, size_t stride, size_t M, int nt) {
+  auto part = [=](size_t a, size_t b) {
+    if (stride == M) memcpy(dst + a * M, src + a * M, (b - a) * M);
+    else
+      for (size_t r = a; r < b; r++) memcpy(dst + r * M, src + r * stride, M);
+  };
+  const size_t T = std::min<size_t>(nt, std::max<size_t>(1, rows * M >> 22));  // >= 4 MiB each
+  if (T <= 1) return part(0, rows);
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < T; i++) th.emplace_back(part, rows * i / T, rows * (i + 1) / T);
+  part(0, rows / T);
+  for (auto &t : th) t.join();
+}
+
+// Worker w's host shard (nw rows) to its device rows m->traces[w] through its two pinned slots:
+// the host copy of slot i overlaps the DMA of slot i ^ 1.  Runs on the worker's own thread.
+int stage_shard(kbz_mctx *m, size_t w, const uint8_t *src, size_t nw, size_t stride,
+                const int8_t *oc, int threads) {
+  const size_t M = m->M, R = m->stage_rows;
+  MHIP(hipSetDevice(m->dev[w]));
+  for (size_t r0 = 0, i = 0; r0 < nw; r0 += R, i++) {
+    const int sl = (int)(i & 1);
+    const size_t cnt = std::min(R, nw - r0);
+    MHIP(hipEventSynchronize(m->ev_slot[sl][w]));  // the slot's previous DMA is done
+    fill_rows(m->pin[sl][w], src + r0 * stride, cnt, stride, M, threads);
+    MHIP(hipMemcpyAsync(m->traces[w] + r0 * M, m->pin[sl][w], cnt * M, hipMemcpyHostToDevice,
+                        m->s[w]));
+    MHIP(hipEventRecord(m->ev_slot[sl][w], m->s[w]));
+  }
+  if (oc && nw) {
+    memcpy(m->pin_oc[w], oc, nw);
+    MHIP(hipMemcpyAsync(m->oc[w], m->pin_oc[w], nw, hipMemcpyHostToDevice, m->s[w]));
+  }
+  return 0;
+}
+
+// The sharded protocol over the workers, on batches already on their devices: worker w holds
+// n[w] rows at traces[w] (stride apart); the batch is worker 0's rows, then worker 1's, ...
+// Results into hnb[w] / h32[w] (device, or null); m->h32[w] stands in when a hash is needed.
+// Ends with each worker's stream and sticky error flags checked.
+int run_protocol(kbz_mctx *m, const uint8_t *const *traces, const size_t *n, size_t stride,
+                 const int8_t *const *outcome, uint8_t *const *hnb, uint32_t *const *h32,
+                 int want) {
   const size_t W = m->W, M = m->M, row = M + 16;
-  std::vector<size_t> lo(W + 1);
-  for (size_t w = 0; w <= W; w++) lo[w] = n * w / W;
-  for (size_t w = 0; w < W; w++)
-    if (lo[w + 1] - lo[w] > m->max_batch) return fail_multi("a shard exceeds max_batch");
-  DevScope keep;
   const bool dr = m->mode == KBZ_MODE_DYNAMORIO;
   const bool hashed = dr || (want & KBZ_WANT_H32);
   std::vector<size_t> nonempty;
   for (size_t w = 0; w < W; w++)
-    if (lo[w + 1] > lo[w]) nonempty.push_back(w);
-  // 1. shards to their devices, pass 1 (+ k_skip); DynamoRIO: each shard's link row and hash pair
+    if (n[w]) nonempty.push_back(w);
+  // 1. pass 1 (+ k_skip) per shard; DynamoRIO: each shard's link row and hash pair
   for (size_t w = 0; w < W; w++) {
-    const size_t nw = lo[w + 1] - lo[w];
     MHIP(hipSetDevice(m->dev[w]));
-    if (nw) {
-      MHIP(hipMemcpy2DAsync(m->traces[w], M, traces + lo[w] * stride, stride, M, nw,
-                            hipMemcpyHostToDevice, m->s[w]));
-      if (outcome)
-        MHIP(hipMemcpyAsync(m->oc[w], outcome + lo[w], nw, hipMemcpyHostToDevice, m->s[w]));
-    }
-    if (kbz_shard_begin(m->ctx[w], nw ? m->traces[w] : nullptr, nw, M, outcome ? m->oc[w] : nullptr,
-                        hashed ? m->h32[w] : nullptr, nullptr, want, m->s[w]))
+    uint32_t *hw = (h32 && h32[w]) ? h32[w] : m->h32[w];
+    if (kbz_shard_begin(m->ctx[w], n[w] ? traces[w] : nullptr, n[w], stride,
+                        (outcome && n[w]) ? outcome[w] : nullptr, hashed ? hw : nullptr, nullptr,
+                        want, m->s[w]))
       return -1;
     if (dr) {
-      if (kbz_shard_last_row(m->ctx[w], m->mine[w], m->s[w]) ||
-          kbz_shard_last_hash(m->ctx[w], (uint32_t *)(m->mine[w] + M), m->s[w]))
-        return -1;
+      if (kbz_shard_exchange_row(m->ctx[w], m->mine[w], m->s[w])) return -1;
       MHIP(hipEventRecord(m->ev_link[w], m->s[w]));
     }
   }
@@ -449,33 +521,107 @@ extern "C" int kbz_triage_batch_devices(kbz_mctx_t *m, const uint8_t *traces, si
     } else if (kbz_shard_link(m->ctx[v], nullptr, nullptr, 1, nullptr, nullptr, m->s[v])) {
       return -1;
     }
-    if (kbz_shard_reduce(m->ctx[v], m->s[v]) ||
-        kbz_shard_aggregate(m->ctx[v], m->agg_mine[v], m->s[v]))
-      return -1;
+    // the aggregate goes straight into this worker's own slot of its gather buffer
+    if (kbz_shard_reduce_into(m->ctx[v], m->agg_all[v] + v * m->ab, m->s[v])) return -1;
     MHIP(hipEventRecord(m->ev_agg[v], m->s[v]));
   }
-  // 3. every worker gathers the aggregates: prefix (earlier shards) and total; resolve; results
+  // 3. every worker gathers the other aggregates, then resolves with the prefix (earlier shards)
+  //    and the total taken from the gathered rows inside the fused tail
   for (size_t v = 0; v < W; v++) {
     MHIP(hipSetDevice(m->dev[v]));
     for (size_t w = 0; w < W; w++) {
+      if (w == v) continue;
       MHIP(hipStreamWaitEvent(m->s[v], m->ev_agg[w], 0));
-      MHIP(xcopy(m->agg_all[v] + w * m->ab, m->dev[v], m->agg_mine[w], m->dev[w], m->ab, m->s[v]));
+      MHIP(xcopy(m->agg_all[v] + w * m->ab, m->dev[v], m->agg_all[w] + w * m->ab, m->dev[w], m->ab,
+                 m->s[v]));
     }
-    if (kbz_or_prefix_total(v ? m->prefix[v] : nullptr, m->total[v], m->agg_all[v], v, W, m->ab,
-                            m->s[v]) ||
-        kbz_shard_finish(m->ctx[v], v ? m->prefix[v] : nullptr, m->total[v], m->hnb[v], m->s[v]))
+    if (kbz_shard_finish_gathered(m->ctx[v], m->agg_all[v], v, W,
+                                  (hnb && hnb[v]) ? hnb[v] : m->hnb[v], m->s[v]))
       return -1;
-    const size_t nw = lo[v + 1] - lo[v];
-    if (nw && hnb_out)
-      MHIP(hipMemcpyAsync(hnb_out + lo[v], m->hnb[v], nw, hipMemcpyDeviceToHost, m->s[v]));
-    if (nw && h32_out && hashed)
-      MHIP(hipMemcpyAsync(h32_out + lo[v], m->h32[v], nw * 4, hipMemcpyDeviceToHost, m->s[v]));
   }
-  for (size_t v = 0; v < W; v++) {
+  return 0;
+}
+
+int check_errors(kbz_mctx *m) {
+  for (size_t v = 0; v < m->W; v++) {
     MHIP(hipSetDevice(m->dev[v]));
     if (kbz_sync(m->ctx[v], m->s[v])) return -1;  // the stream, then the sticky error flags
   }
   return 0;
+}
+}  // namespace
+
+extern "C" int kbz_triage_batch_devices(kbz_mctx_t *m, const uint8_t *traces, size_t n,
+                                        size_t stride, const int8_t *outcome, uint8_t *hnb_out,
+                                        uint32_t *h32_out, int want) {
+  if (!m) return fail_multi("null mctx");
+  if (n && (!traces || stride < m->M)) return fail_multi("bad traces / stride");
+  if (want & KBZ_WANT_X64) return fail_multi("kbz_triage_batch_devices: XXH64 is not gathered");
+  const size_t W = m->W, M = m->M;
+  std::vector<size_t> lo(W + 1), cnt(W);
+  for (size_t w = 0; w <= W; w++) lo[w] = n * w / W;
+  for (size_t w = 0; w < W; w++) {
+    cnt[w] = lo[w + 1] - lo[w];
+    if (cnt[w] > m->max_batch) return fail_multi("a shard exceeds max_batch");
+  }
+  DevScope keep;
+  const bool hashed = m->mode == KBZ_MODE_DYNAMORIO || (want & KBZ_WANT_H32);
+  // 1. every worker stages its shard on its own host thread (pinned slots, DMA overlapped with the
+  //    next slot's host copy); the copy threads of a slot are shared out over the workers
+  const int per = std::max(1, 8 / (int)W);
+  std::vector<int> rc(W, 0);
+  std::vector<std::string> err(W);
+  auto job = [&](size_t w) {
+    if (stage_shard(m, w, traces + lo[w] * stride, cnt[w], stride, outcome ? outcome + lo[w] : nullptr,
+                    per)) {
+      rc[w] = -1;
+      err[w] = kbz_last_error();
+    }
+  };
+  if (W == 1) {
+    job(0);
+  } else {
+    std::vector<std::thread> th;
+    for (size_t w = 0; w < W; w++) th.emplace_back(job, w);
+    for (auto &t : th) t.join();
+  }
+  for (size_t w = 0; w < W; w++)
+    if (rc[w]) return fail_multi("staging shard " + std::to_string(w) + ": " + err[w]);
+  std::vector<const uint8_t *> tp(W);
+  std::vector<const int8_t *> op(W);
+  for (size_t w = 0; w < W; w++) {
+    tp[w] = m->traces[w];
+    op[w] = outcome ? m->oc[w] : nullptr;
+  }
+  if (run_protocol(m, tp.data(), cnt.data(), M, outcome ? op.data() : nullptr, nullptr, nullptr,
+                   want))
+    return -1;
+  // 2. results to the host, per worker on its stream
+  for (size_t v = 0; v < W; v++) {
+    MHIP(hipSetDevice(m->dev[v]));
+    if (cnt[v] && hnb_out)
+      MHIP(hipMemcpyAsync(hnb_out + lo[v], m->hnb[v], cnt[v], hipMemcpyDeviceToHost, m->s[v]));
+    if (cnt[v] && h32_out && hashed)
+      MHIP(hipMemcpyAsync(h32_out + lo[v], m->h32[v], cnt[v] * 4, hipMemcpyDeviceToHost, m->s[v]));
+  }
+  return check_errors(m);
+}
+
+extern "C" int kbz_triage_batch_devices_resident(kbz_mctx_t *m, const uint8_t *const *traces,
+                                                 const size_t *n, size_t stride,
+                                                 const int8_t *const *outcome,
+                                                 uint8_t *const *hnb_out, uint32_t *const *h32_out,
+                                                 int want) {
+  if (!m || !n) return fail_multi("null argument");
+  if (want & KBZ_WANT_X64) return fail_multi("kbz_triage_batch_devices: XXH64 is not gathered");
+  if (stride < m->M || stride % 16) return fail_multi("stride must be >= map_size and a multiple of 16");
+  for (size_t w = 0; w < m->W; w++) {
+    if (n[w] > m->max_batch) return fail_multi("a shard exceeds max_batch");
+    if (n[w] && (!traces || !traces[w])) return fail_multi("null traces for a non-empty shard");
+  }
+  DevScope keep;
+  if (run_protocol(m, traces, n, stride, outcome, hnb_out, h32_out, want)) return -1;
+  return check_errors(m);
 }
 
 extern "C" int kbz_mctx_get_virgin(kbz_mctx_t *m, uint8_t *host_out) {

@@ -2255,6 +2255,10 @@ __device__ __forceinline__ void fix_column(const FixArgs &f, uint32_t map_size, 
 // Per column (8 B per thread): [DynamoRIO: fix path first], then segprev[s] = OR of segments
 // < s (local exclusive prefix), total = OR of all segments; segor is re-zeroed for the next
 // batch.
+// KEEP (the sharded protocol's fused finish, kbz_shard_reduce_into): only the fix path and the
+// total -- the segment ORs stay for k_tail, which takes its prefixes from them and zeroes the
+// other buffer, and `total` is the caller's exchange buffer.
+template <bool KEEP>
 __global__ __launch_bounds__(256) void k_total(uint8_t *segor, uint32_t nseg, int nclass,
                                                 uint32_t map_size, uint8_t *segprev,
                                                 uint8_t *total, FixArgs fix) {
@@ -2271,12 +2275,23 @@ __global__ __launch_bounds__(256) void k_total(uint8_t *segor, uint32_t nseg, in
   for (int s = 0; s < kMaxSeg; s++) {
     if (s < (int)nseg) {
       const size_t off = ((size_t)s * nclass + k) * map_size + col;
-      *(uint64_t *)(segprev + off) = acc;
-      *(uint64_t *)(segor + off) = 0;  // ready for the next batch
+      if (!KEEP) {
+        *(uint64_t *)(segprev + off) = acc;
+        *(uint64_t *)(segor + off) = 0;  // ready for the next batch
+      }
       acc |= v[s];
     }
   }
   *(uint64_t *)(total + (size_t)k * map_size + col) = acc;
+}
+
+// The sharded protocol's link exchange in one launch: this shard's last row (if any) and its
+// hash pair {last hash32, flags} -> out[0 .. M) and out[M .. M + 8).
+__global__ __launch_bounds__(256) void k_exch(const uint8_t *row, uint32_t M,
+                                               const uint32_t *pair, uint8_t *out) {
+  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (row && i < M) *(uint4 *)(out + i) = *(const uint4 *)(row + i);
+  if (blockIdx.x == 0 && threadIdx.x < 2) ((uint32_t *)(out + M))[threadIdx.x] = pair[threadIdx.x];
 }
 
 #ifndef KBZ_SCAN_ILP  // chunk rows k_scan loads per round trip: 8 beat 16 and 32 on fresh config-2
@@ -2876,6 +2891,12 @@ struct TailArgs {
   uint32_t *flags_w, *fix_list_w, *fix_cnt_w;  // the walks' fix list (DynamoRIO)
   const uint8_t *copy_src;  // the batch's last row -> the context's saved row (when pass 1 ran
   uint8_t *copy_dst;        // k_skip's rule, k_skip's copy blocks' role), or null
+  // a shard of the sharded protocol (kbz_shard_finish_gathered): k_chain and k_total<true> ran
+  // (walks, fix path, bookkeeping); the prefix of the earlier shards and the batch total come
+  // from the all-gathered aggregates [world][nclass * map_size]
+  uint32_t shard;
+  const uint8_t *gathered;
+  uint32_t rank, world;
 };
 #ifndef KBZ_TAIL_INLINE_MAX  // claimed bytes one k_tail wave resolves inline; the rest become
 #define KBZ_TAIL_INLINE_MAX 16  // items, dealt over all of k_fin's waves.  Fresh batches on a warm
@@ -2965,8 +2986,10 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
     for (uint32_t ss = s; ss < kMaxSeg; ss += a.nseg)
       *(uint4 *)(a.segor_next + ((size_t)ss * a.nclass + k) * M + col) = make_uint4(0, 0, 0, 0);
   // ---- 1. DynamoRIO chain / fix path -------------------------------------------------------
-  const uint32_t nbad = dr ? a.counters[4] : 0u, bad0 = dr ? a.tail[4] : 0u;
-  if (dr && wg0 && threadIdx.x == 0) {  // k_chain's bookkeeping for a one-shard batch
+  // (a shard: k_chain walked its bad rows and k_total<true> ran the fix path already)
+  const uint32_t nbad = (dr && !a.shard) ? a.counters[4] : 0u;
+  const uint32_t bad0 = (dr && !a.shard) ? a.tail[4] : 0u;
+  if (dr && !a.shard && wg0 && threadIdx.x == 0) {  // k_chain's bookkeeping for a one-shard batch
     const uint32_t f = a.shard_last[1];
     *a.next_last = f ? a.shard_last[0] : *a.ctx_last;
     *a.saved_ok = (nbad == 0) && ((f & 4u) || !bad0);
@@ -3032,6 +3055,18 @@ __global__ __launch_bounds__(256) void k_tail(TailArgs a) {
         if (ss < s) prev = or4(prev, sv[q]);
         if (ss <= s) send = or4(send, sv[q]);
       }
+    }
+    if (a.gathered) {  // a shard: + the earlier shards' coverage; V' from the batch total
+      const size_t ab = (size_t)a.nclass * M;
+      uint4 pre = make_uint4(0, 0, 0, 0), all = pre;
+      for (uint32_t r = 0; r < a.world; r++) {
+        const uint4 g = *(const uint4 *)(a.gathered + r * ab + kc);
+        if (r < a.rank) pre = or4(pre, g);
+        all = or4(all, g);
+      }
+      prev = or4(prev, pre);
+      send = or4(send, pre);
+      tot = all;
     }
     const uint4 vir = *(const uint4 *)(a.vcur + kc);
     const uint4 ig = *(const uint4 *)((a.ignore ? a.ignore : a.vcur) + col);
@@ -3739,6 +3774,7 @@ struct kbz_ctx {
   uint8_t *segor_alt = nullptr;  // the other buffer (the fused tail zeroes it and swaps)
   uint32_t *tail = nullptr;      // k_tail's words (kTailFixDone + column groups)
   bool fused_ok = true;          // one-shard batches through k_tail (KBZ_DEBUG_STAGED=1: staged)
+  bool shard_keep = false;       // this batch's k_total kept the segment ORs (kbz_shard_reduce_into)
   bool rec_ok = true;            // pass-1 claim records (KBZ_DEBUG_NO_REC=1: off)
   uint64_t *frec = nullptr;      // [max_chunks][M] claim records, allocated on first use
   uint64_t *rflags = nullptr;    // [max_chunks][nfw] tiles with records
@@ -4323,6 +4359,7 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
     // kbz_shard_link may already have marked this batch's last row as the next row-0
     // predecessor, but V never received that batch: forget the row
     c->saved_valid = false;
+    c->shard_keep = false;
     c->stage = 0;
   }
   c->cur_traces = traces;
@@ -4411,13 +4448,15 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
   // DynamoRIO: pass 1's stop event is the start of k_skip, its successor on the stream (a stop
   // event on pass 1's own dispatch left 4.8 us of idle GPU after it, profiles/r05_evgap; the
   // interval now also holds the boundary, so the pass-1 time is an upper bound)
-  const bool stop_on_skip = pev.start && c->mode == KBZ_MODE_DYNAMORIO && KBZ_P1_STOP_ON_NEXT;
-  P1Ev pev1 = pev;
-  if (stop_on_skip) pev1.stop = nullptr;
   // a fused DynamoRIO batch through k_pass1s: the kernel runs k_skip's rule itself (its row-0 and
   // saved-row roles included); the copy of the last row into the context goes to k_tail
   const bool fsk = c->mode == KBZ_MODE_DYNAMORIO && c->fskip_ok &&
                    !pass1_is_wide(c->pass1, c->cur_chunks);
+  // (no k_skip launch when pass 1 runs the rule itself: the stop event stays on pass 1)
+  const bool stop_on_skip =
+      pev.start && c->mode == KBZ_MODE_DYNAMORIO && KBZ_P1_STOP_ON_NEXT && !fsk;
+  P1Ev pev1 = pev;
+  if (stop_on_skip) pev1.stop = nullptr;
   c->tail_copy_src = nullptr;
   c->tail_copy_dst = nullptr;
   if (fsk) {  // (a shard of the sharded protocol: rows j >= 1 only, k_chain links row 0)
@@ -4671,6 +4710,7 @@ int kbz_shard_reduce(kbz_ctx_t *c, void *stream) {
   if (!c || c->stage != 2) return fail("kbz_shard_reduce: call kbz_shard_link first");
   DevGuard g(c->device);
   hipStream_t s = (hipStream_t)stream;
+  c->shard_keep = false;
   if (c->cur_n == 0) {
     HIP_TRY(hipMemsetAsync(c->total, 0, c->nc * c->M, s));
     HIP_TRY(hipMemsetAsync(c->segprev, 0, c->nc * c->M, s));
@@ -4693,7 +4733,7 @@ int kbz_shard_reduce(kbz_ctx_t *c, void *stream) {
     }
     hipEvent_t st0;
     if (stage_begin(c, s, &st0)) return -1;
-    hipLaunchKernelGGL(k_total, dim3(cdiv(c->M / 8, 256), 1, c->nc), dim3(256), 0, s, c->segor,
+    hipLaunchKernelGGL(k_total<false>, dim3(cdiv(c->M / 8, 256), 1, c->nc), dim3(256), 0, s, c->segor,
                        c->cur_nseg, c->nc, (uint32_t)c->M, c->segprev, c->total, fx);
     HIP_TRY(hipGetLastError());
     if (stage_end(c, s, KBZ_STAGE_REDUCE, st0)) return -1;
@@ -4715,6 +4755,8 @@ size_t kbz_shard_aggregate_bytes(kbz_ctx_t *c) { return c ? c->nc * c->M : 0; }
 int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, uint8_t *hnb_out,
                      void *stream) {
   if (!c || c->stage != 3) return fail("kbz_shard_finish: call kbz_shard_reduce first");
+  if (c->shard_keep) return fail("kbz_shard_finish: after kbz_shard_reduce_into, finish with "
+                                 "kbz_shard_finish_gathered");
   if (!total) total = c->total;  // single shard: its own aggregate is the total
   DevGuard g(c->device);
   hipStream_t s = (hipStream_t)stream;
@@ -4758,6 +4800,141 @@ int kbz_shard_finish(kbz_ctx_t *c, const uint8_t *prefix, const uint8_t *total, 
     HIP_TRY(hipMemsetAsync(c->shard_last, 0, 2 * sizeof(uint32_t), s));
   }
   c->vcur = vn;
+  c->stage = 0;
+  return 0;
+}
+
+int kbz_shard_exchange_row(kbz_ctx_t *c, uint8_t *d_out, void *stream) {
+  if (!c || !d_out) return fail("null argument");
+  if (c->stage < 1) return fail("kbz_shard_exchange_row: call kbz_shard_begin first");
+  if (((uintptr_t)d_out | c->M) & 15) return fail("kbz_shard_exchange_row: d_out must be 16-B aligned");
+  DevGuard g(c->device);
+  const uint8_t *row = c->cur_n ? c->cur_traces + (c->cur_n - 1) * c->cur_stride : nullptr;
+  hipLaunchKernelGGL(k_exch, dim3(cdiv(c->M / 16, 256)), dim3(256), 0, (hipStream_t)stream, row,
+                     (uint32_t)c->M, c->shard_last, d_out);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int kbz_shard_reduce_into(kbz_ctx_t *c, uint8_t *d_aggregate, void *stream) {
+  if (!c || !d_aggregate) return fail("null argument");
+  if (c->stage != 2) return fail("kbz_shard_reduce_into: call kbz_shard_link first");
+  if ((uintptr_t)d_aggregate & 7) return fail("kbz_shard_reduce_into: d_aggregate must be 8-B aligned");
+  DevGuard g(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (c->cur_n == 0) {
+    HIP_TRY(hipMemsetAsync(d_aggregate, 0, c->nc * c->M, s));
+  } else {
+    FixArgs fx{};
+    if (c->fix_pending) {
+      fx.traces = c->cur_traces;
+      fx.stride = c->cur_stride;
+      fx.n = (uint32_t)c->cur_n;
+      fx.skip = c->skip;
+      fx.fix_list = c->fix_list;
+      fx.fix_cnt = c->counters + 3;
+      fx.chunk_or = c->chunk_or;
+      fx.chunk_cls = c->chunk_cls;
+      fx.nchunks = c->cur_chunks;
+      fx.seg_len = c->cur_seg_len;
+      fx.listed = c->flags;
+      fx.tflags = c->tflags;
+      fx.nfw = c->nfw;
+    }
+    hipEvent_t st0;
+    if (stage_begin(c, s, &st0)) return -1;
+    hipLaunchKernelGGL(k_total<true>, dim3(cdiv(c->M / 8, 256), 1, c->nc), dim3(256), 0, s,
+                       c->segor, c->cur_nseg, c->nc, (uint32_t)c->M, nullptr, d_aggregate, fx);
+    HIP_TRY(hipGetLastError());
+    if (stage_end(c, s, KBZ_STAGE_REDUCE, st0)) return -1;
+  }
+  c->shard_keep = true;
+  c->stage = 3;
+  return 0;
+}
+
+int kbz_shard_finish_gathered(kbz_ctx_t *c, const uint8_t *d_gathered, size_t rank, size_t world,
+                              uint8_t *hnb_out, void *stream) {
+  if (!c || !d_gathered) return fail("null argument");
+  if (c->stage != 3 || !c->shard_keep)
+    return fail("kbz_shard_finish_gathered: call kbz_shard_reduce_into first");
+  if (world == 0 || rank >= world) return fail("kbz_shard_finish_gathered: rank >= world");
+  if (((uintptr_t)d_gathered | (c->nc * c->M)) & 15)
+    return fail("kbz_shard_finish_gathered: d_gathered must be 16-B aligned");
+  DevGuard g(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  const bool dr = c->mode == KBZ_MODE_DYNAMORIO;
+  const uint32_t n = (uint32_t)c->cur_n, M = (uint32_t)c->M;
+  const uint8_t *ign = dr ? c->ignore : nullptr;
+  const uint8_t *skip = dr ? c->skip : nullptr;
+  const int vn = c->vcur ^ 1;
+  TailArgs a{};
+  a.ca = ClaimArgs{c->cur_traces, c->cur_stride, n, c->mode, c->cur_outcome, skip, c->hnb32,
+                   c->counters + 2};
+  a.ra = ResolveArgs{c->cur_traces, c->cur_stride, n, c->mode, c->cur_outcome, skip, c->hnb32,
+                     c->counters + 2, c->chunk_or, c->nc, M, c->V[c->vcur], ign};
+  a.fx = FixArgs{c->cur_traces, c->cur_stride, n, c->skip, c->fix_list, c->counters + 3,
+                 c->chunk_or, c->chunk_cls, c->cur_chunks, c->cur_seg_len, c->flags, c->tflags,
+                 c->nfw};
+  a.chunk_or = c->chunk_or;
+  a.chunk_cls = c->chunk_cls;
+  a.nchunks = c->cur_chunks;
+  a.seg_len = c->cur_seg_len;
+  a.nseg = c->cur_nseg;
+  a.nclass = c->nc;
+  a.map_size = M;
+  a.segor = c->segor;
+  a.segor_next = c->segor_alt;
+  a.vcur = c->V[c->vcur];
+  a.vnext = c->V[vn];
+  a.ignore = ign;
+  a.items = c->items;
+  a.cap = c->item_cap;
+  a.counters = c->counters;
+  a.tflags = c->tflags;
+  a.nfw = c->nfw;
+  a.listed = dr ? c->flags : nullptr;
+  a.win_items = c->win_items;
+  a.inline_max = c->inline_max;
+  a.tail = c->tail;
+  a.frec = nullptr;  // shards record no claims in pass 1
+  a.shard_last = c->shard_last;
+  a.neq = c->neq;
+  a.bad_list = c->bad_list;
+  a.flags_w = c->flags;
+  a.fix_list_w = c->fix_list;
+  a.fix_cnt_w = c->counters + 3;
+  a.shard = 1;
+  a.gathered = d_gathered;
+  a.rank = (uint32_t)rank;
+  a.world = (uint32_t)world;
+  hipEvent_t st0;
+  if (stage_begin(c, s, &st0)) return -1;
+  const unsigned ncg = cdiv(M / 16, 256);
+  hipLaunchKernelGGL(k_tail, dim3(ncg, c->cur_nseg, c->nc), dim3(256), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  if (stage_end(c, s, KBZ_STAGE_SCAN, st0)) return -1;
+  FinArgs f{};
+  f.ra = a.ra;
+  f.items = c->items;
+  f.cap = c->item_cap;
+  f.counters = c->counters;
+  f.tail = c->tail;
+  f.tail_fix_words = ncg;
+  f.hnb_out = hnb_out;
+  f.err_out = c->d_err;
+  f.shard_last = c->shard_last;
+  f.flags_w = c->flags;
+  f.fix_list_w = c->fix_list;
+  f.fix_cnt = dr ? c->counters + 3 : nullptr;
+  f.nchunks = c->cur_chunks;
+  if (stage_begin(c, s, &st0)) return -1;
+  hipLaunchKernelGGL(k_fin, dim3(512), dim3(256), 0, s, f);
+  HIP_TRY(hipGetLastError());
+  if (stage_end(c, s, KBZ_STAGE_RESOLVE, st0)) return -1;
+  std::swap(c->segor, c->segor_alt);
+  c->vcur = vn;
+  c->shard_keep = false;
   c->stage = 0;
   return 0;
 }

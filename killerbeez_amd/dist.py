@@ -9,13 +9,18 @@ the OR of the coverage seen by the ranks before it:
      map_size per rank); the first trace of a shard is compared with the last trace of the
      nearest non-empty earlier shard (hash for the skip rule, row for its exactness), and every
      rank remembers the batch's last row for the next batch
-  3. local OR aggregate per virgin map (kbz_shard_reduce)
+  3. local OR aggregate per virgin map (kbz_shard_reduce_into: straight into the buffer the
+     all-gather sends)
   4. all-gather of the aggregates (nclass * map_size bytes per rank) -> prefix = OR of earlier
      ranks, total = OR of all ranks.  RCCL has no bitwise reductions, so this is an
-     all-gather plus one local OR pass for both (kbz_or_prefix_total), ~8 x 64 KiB over xGMI:
-     latency-bound.
-  5. local resolve with the prefix; every rank applies V' = V & ~total, so the virgin maps
-     stay identical on all ranks.
+     all-gather; the OR of the gathered rows happens inside the resolve (~8 x 64 KiB over xGMI:
+     latency-bound).
+  5. local resolve with the prefix (kbz_shard_finish_gathered: the one-shard batch's fused tail,
+     k_tail + k_fin); every rank applies V' = V & ~total, so the virgin maps stay identical on
+     all ranks.
+Engines without the fused finish (the tests' CPU engine) run the same steps with separate
+aggregate copy, prefix / total pass and finish (kbz_shard_reduce, kbz_or_prefix_total,
+kbz_shard_finish).
 
 The engine is any object with the shard_* methods of killerbeez_amd.triage.TriageContext
 (tests plug a CPU engine in to exercise this protocol with the gloo backend).
@@ -80,6 +85,9 @@ def triage_sharded(engine, traces, outcome, counts, rank, world, want=1, group=N
     device = device if device is not None else traces.device
     clk = _Clock(device) if timings is not None else None
     mark = clk.mark if clk else (lambda name: None)
+    # engines with the fused finish (TriageContext): one launch for the link exchange, the
+    # aggregate written into its all-gather slot, prefix / total taken inside the fused tail
+    fused = hasattr(engine, "shard_finish_gathered")
     mark("start")
     out = engine.shard_begin(traces, outcome, want)
     mark("pass1")
@@ -89,8 +97,11 @@ def triage_sharded(engine, traces, outcome, counts, rank, world, want=1, group=N
         # [last row | hash pair | pad]: map_size + 16 bytes, so every gathered row stays
         # 16-byte aligned (k_chain reads rows with 16-byte loads)
         buf = torch.zeros(m + 16, dtype=torch.uint8, device=device)
-        engine.shard_last_row(buf[:m])
-        engine.shard_last_hash(buf[m:m + 8].view(torch.int32))
+        if fused:
+            engine.shard_exchange_row(buf)
+        else:
+            engine.shard_last_row(buf[:m])
+            engine.shard_last_hash(buf[m:m + 8].view(torch.int32))
         mark("link")
         bufs = _all_gather(buf, world, group) if coll else buf.view(1, -1)
         mark("collective")
@@ -104,8 +115,20 @@ def triage_sharded(engine, traces, outcome, counts, rank, world, want=1, group=N
     else:
         engine.shard_link(None, None, True, None, None)
     mark("link")
-    engine.shard_reduce()
     nb = engine.shard_aggregate_bytes()
+    if fused:
+        agg = torch.empty(nb, dtype=torch.uint8, device=device)
+        engine.shard_reduce_into(agg)
+        mark("reduce")
+        allagg = _all_gather(agg, world, group) if coll else agg.view(1, nb)
+        if coll:
+            mark("collective")
+        res = engine.shard_finish_gathered(allagg, rank if coll else 0, world if coll else 1)
+        mark("finish")
+        if clk is not None:
+            timings.append(clk)
+        return res
+    engine.shard_reduce()
     agg = torch.empty(nb, dtype=torch.uint8, device=device)
     engine.shard_aggregate(agg)
     mark("reduce")

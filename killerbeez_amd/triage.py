@@ -310,6 +310,31 @@ class TriageContext:
                                      _stream_handle(stream)), "kbz_shard_finish")
         return out
 
+    # the protocol with fewer launches per step (include/kbz_triage.h, round 6)
+    def shard_exchange_row(self, out, stream=None):
+        """This shard's last raw trace and hash pair into CUDA uint8 out[map_size + 8 ...]: the
+        row at [0, map_size), the int32 pair at [map_size, map_size + 8); one launch."""
+        check(lib().kbz_shard_exchange_row(self._h, C.c_void_p(out.data_ptr()),
+                                           _stream_handle(stream)), "kbz_shard_exchange_row")
+        return out
+
+    def shard_reduce_into(self, out, stream=None):
+        """Fix path + this shard's OR aggregate straight into CUDA uint8 out[nclass*map_size]
+        (e.g. this rank's slot of the all-gather buffer)."""
+        check(lib().kbz_shard_reduce_into(self._h, C.c_void_p(out.data_ptr()),
+                                          _stream_handle(stream)), "kbz_shard_reduce_into")
+        return out
+
+    def shard_finish_gathered(self, gathered, rank, world, stream=None):
+        """Resolve with the prefix / total of the all-gathered aggregates
+        (CUDA uint8 [world, nclass*map_size]) inside the fused tail."""
+        out = self._out
+        check(lib().kbz_shard_finish_gathered(self._h, C.c_void_p(gathered.data_ptr()), rank,
+                                              world, C.c_void_p(out["hnb"].data_ptr()),
+                                              _stream_handle(stream)),
+              "kbz_shard_finish_gathered")
+        return out
+
     @staticmethod
     def or_reduce(out, stacked, r_lo, r_hi, nbytes, stream=None):
         return or_reduce(out, stacked, r_lo, r_hi, nbytes, stream)
@@ -431,6 +456,46 @@ class MultiTriageContext:
                                              None if oc is None else _np_ptr(oc), _np_ptr(hnb),
                                              _np_ptr(h32), want), "kbz_triage_batch_devices")
         return {"hnb": hnb, "h32": h32}
+
+    def peer_pairs(self) -> int:
+        """Ordered pairs of the workers' distinct devices with peer access enabled."""
+        return lib().kbz_mctx_peer_pairs(self._h)
+
+    def triage_resident(self, shards, outcomes=None, want: int = WANT_H32):
+        """A batch already on the devices: shards[w] is worker w's uint8 [n_w, map_size] tensor
+        on its device (the batch is shard 0's rows, then shard 1's, ...), outcomes[w] its int8
+        [n_w] tensor (or None).  Returns per-worker device tensors {"hnb": [...], "h32": [...]}."""
+        import torch
+
+        W = self.workers()
+        if len(shards) != W or (outcomes is not None and len(outcomes) != W):
+            raise ValueError(f"one shard (and outcome) per worker ({W})")
+        ptrs = (C.c_void_p * W)()
+        ops = (C.c_void_p * W)()
+        hp = (C.c_void_p * W)()
+        h3 = (C.c_void_p * W)()
+        ns = (C.c_size_t * W)()
+        hnb, h32 = [], []
+        for w, t in enumerate(shards):
+            if t.dim() != 2 or t.shape[1] != self.map_size or t.dtype != torch.uint8 or \
+                    not t.is_contiguous():
+                raise ValueError("each shard: a contiguous uint8 [n, map_size] tensor")
+            ns[w] = t.shape[0]
+            ptrs[w] = t.data_ptr() if t.shape[0] else None
+            if outcomes is not None:
+                o = outcomes[w]
+                if o.dtype != torch.int8 or o.shape[0] != t.shape[0]:
+                    raise ValueError("each outcome: int8 [n] on its shard's device")
+                ops[w] = o.data_ptr() if t.shape[0] else None
+            hnb.append(torch.empty(max(1, t.shape[0]), dtype=torch.uint8, device=t.device))
+            h32.append(torch.empty(max(1, t.shape[0]), dtype=torch.int32, device=t.device))
+            hp[w], h3[w] = hnb[-1].data_ptr(), h32[-1].data_ptr()
+        check(lib().kbz_triage_batch_devices_resident(
+            self._h, C.cast(ptrs, C.c_void_p), C.cast(ns, C.c_void_p), self.map_size,
+            None if outcomes is None else C.cast(ops, C.c_void_p), C.cast(hp, C.c_void_p),
+            C.cast(h3, C.c_void_p), want), "kbz_triage_batch_devices_resident")
+        return {"hnb": [h[:shards[w].shape[0]] for w, h in enumerate(hnb)],
+                "h32": [h[:shards[w].shape[0]] for w, h in enumerate(h32)]}
 
     def get_virgin(self) -> np.ndarray:
         v = np.empty((3, self.map_size), np.uint8)

@@ -129,7 +129,29 @@ class CpuShardEngine:
         return {"hnb": torch.from_numpy(r["hnb"])}
 
 
-def _worker(rank, world, port, mode, counts, seed, q):
+class CpuShardEngineFused(CpuShardEngine):
+    """The fused-finish engine API (shard_exchange_row, shard_reduce_into,
+    shard_finish_gathered: what TriageContext offers and dist.triage_sharded prefers), built
+    from the steps it replaces -- so the gloo runs cover both protocol branches of dist.py."""
+
+    def shard_exchange_row(self, out):
+        self.shard_last_row(out[:M])
+        self.shard_last_hash(out[M:M + 8].view(torch.int32))
+        return out
+
+    def shard_reduce_into(self, out):
+        self.shard_reduce()
+        return self.shard_aggregate(out)
+
+    def shard_finish_gathered(self, gathered, rank, world):
+        nb = self.shard_aggregate_bytes()
+        total = torch.empty(nb, dtype=torch.uint8)
+        prefix = torch.empty(nb, dtype=torch.uint8) if rank > 0 else None
+        self.or_prefix_total(prefix, total, gathered, rank, world, nb)
+        return self.shard_finish(prefix, total)
+
+
+def _worker(rank, world, port, mode, counts, seed, q, fused=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     t, oc = synth.sparse_np(sum(counts), M, seed=seed, hot_frac=0.05)
@@ -137,7 +159,7 @@ def _worker(rank, world, port, mode, counts, seed, q):
     if sum(counts) > 51:
         t[51] = t[50]
     lo = sum(counts[:rank])
-    eng = CpuShardEngine(mode, np.full((3, M), 0xFF, np.uint8))
+    eng = (CpuShardEngineFused if fused else CpuShardEngine)(mode, np.full((3, M), 0xFF, np.uint8))
     hnbs, timings = [], []
     for batch in range(2):  # two consecutive sharded batches: state carries over
         tt = t if batch == 0 else t[::-1].copy()
@@ -160,14 +182,15 @@ def _free_port():
     return p
 
 
+@pytest.mark.parametrize("fused", [False, True], ids=["staged", "fused-finish"])
 @pytest.mark.parametrize("mode", [oracle.MODE_AFL, oracle.MODE_DYNAMORIO])
 @pytest.mark.parametrize("counts", [[60, 40], [50, 0, 47]])
-def test_sharded_equals_sequential(oracle_lib, mode, counts):
+def test_sharded_equals_sequential(oracle_lib, mode, counts, fused):
     world = len(counts)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, counts, 7, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, counts, 7, q, fused))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -299,9 +299,10 @@ def test_full_size_config2(gpu):
     np.testing.assert_array_equal(ctx.get_virgin(), v)
 
 
-def _run_shards(ctxs, shards, ocs, mode, device):
+def _run_shards(ctxs, shards, ocs, mode, device, fused=False):
     """One sharded batch over in-process 'ranks' (one context each, same GPU), phase by phase
-    as killerbeez_amd.dist.triage_sharded runs them, with the all-gathers done locally."""
+    as killerbeez_amd.dist.triage_sharded runs them, with the all-gathers done locally.
+    fused: the round-6 steps (shard_exchange_row, shard_reduce_into, shard_finish_gathered)."""
     import torch
 
     world = len(ctxs)
@@ -310,10 +311,22 @@ def _run_shards(ctxs, shards, ocs, mode, device):
     nonempty = [r for r in range(world) if counts[r] > 0]
     if mode == MODE_DYNAMORIO:
         m = ctxs[0].map_size
-        pairs = torch.stack([c.shard_last_hash(torch.empty(2, dtype=torch.int32, device=device))
-                             for c in ctxs])
-        rows = torch.stack([c.shard_last_row(torch.zeros(m, dtype=torch.uint8, device=device))
-                            for c in ctxs])
+        if fused:
+            bufs = torch.stack([c.shard_exchange_row(torch.zeros(m + 16, dtype=torch.uint8,
+                                                                 device=device)) for c in ctxs])
+            rows, pairs = bufs[:, :m], bufs[:, m:m + 8].contiguous().view(torch.int32)
+            # the one-launch exchange equals the two copies it replaces
+            for r, c in enumerate(ctxs):
+                p2 = c.shard_last_hash(torch.empty(2, dtype=torch.int32, device=device))
+                assert torch.equal(p2, pairs[r])
+                if counts[r]:
+                    r2 = c.shard_last_row(torch.zeros(m, dtype=torch.uint8, device=device))
+                    assert torch.equal(r2, rows[r])
+        else:
+            pairs = torch.stack([c.shard_last_hash(torch.empty(2, dtype=torch.int32,
+                                                               device=device)) for c in ctxs])
+            rows = torch.stack([c.shard_last_row(torch.zeros(m, dtype=torch.uint8,
+                                                             device=device)) for c in ctxs])
         for r, c in enumerate(ctxs):
             prev = [q for q in nonempty if q < r]
             p = prev[-1] if prev else None
@@ -324,9 +337,19 @@ def _run_shards(ctxs, shards, ocs, mode, device):
     else:
         for c in ctxs:
             c.shard_link(None, None, True, None, None)
+    nb = ctxs[0].shard_aggregate_bytes()
+    if fused:
+        allagg = torch.empty(world, nb, dtype=torch.uint8, device=device)
+        for r, c in enumerate(ctxs):
+            c.shard_reduce_into(allagg[r])
+        res = [c.shard_finish_gathered(allagg, r, world) for r, c in enumerate(ctxs)]
+        torch.cuda.synchronize()
+        for c in ctxs:
+            c.sync()
+        return (np.concatenate([o["hnb"].cpu().numpy() for o in res]),
+                np.concatenate([o["h32"].cpu().numpy().view(np.uint32) for o in res]))
     for c in ctxs:
         c.shard_reduce()
-    nb = ctxs[0].shard_aggregate_bytes()
     allagg = torch.stack([c.shard_aggregate(torch.empty(nb, dtype=torch.uint8, device=device))
                           for c in ctxs])
     res = []
@@ -351,7 +374,8 @@ def _run_shards(ctxs, shards, ocs, mode, device):
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("counts", [[700, 324], [640, 0, 193, 64]])
-def test_sharded_protocol_on_gpu(gpu, mode, counts):
+@pytest.mark.parametrize("fused", [False, True], ids=["staged-finish", "fused-finish"])
+def test_sharded_protocol_on_gpu(gpu, mode, counts, fused):
     """The multi-GPU protocol (dist.py) through the C ABI: shard aggregates (restricted to
     still-virgin bits), prefix/total ORs and the last-hash links give the sequential result,
     batch after batch (the second batch adds new coverage to carried virgin maps)."""
@@ -372,7 +396,7 @@ def test_sharded_protocol_on_gpu(gpu, mode, counts):
             shards.append(torch.from_numpy(t[lo:lo + c].copy()).cuda())
             ocs.append(torch.from_numpy(oc[lo:lo + c].copy()).cuda())
             lo += c
-        hnb, h32 = _run_shards(ctxs, shards, ocs, mode, torch.device("cuda"))
+        hnb, h32 = _run_shards(ctxs, shards, ocs, mode, torch.device("cuda"), fused)
         np.testing.assert_array_equal(hnb, exp["hnb"])
         np.testing.assert_array_equal(h32, exp["h32"])
         for c in ctxs:
@@ -381,6 +405,47 @@ def test_sharded_protocol_on_gpu(gpu, mode, counts):
                 assert c.last_hash == exp["last_hash"]
         v, last = exp["virgin"], exp.get("last_hash", 0)
         assert batch == 0 or 0 < (hnb > 0).sum() < n  # later batches still find something
+
+
+@pytest.mark.parametrize("fused", [False, True], ids=["staged-finish", "fused-finish"])
+def test_sharded_protocol_collisions(gpu, fused):
+    """DynamoRIO shards with ignore bytes: hash collisions (equal hash32_with_ignore, different
+    examined bytes) inside a shard, at a shard's row 0 against the previous shard's last row,
+    and a chain of repeats of a collided row across a chunk boundary -- the fix path and the
+    chain walks of k_chain / k_total ahead of either finish."""
+    import torch
+
+    m = 4096
+    rng = np.random.default_rng(3121)
+    counts = [300, 257, 200]
+    n = sum(counts)
+    ign = np.where(rng.random(m) < 0.4, 0, rng.integers(1, 256, size=m)).astype(np.uint8)
+    zc = np.nonzero(ign == 0)[0]
+    ctxs = [TriageContext(m, MODE_DYNAMORIO, c) for c in counts]
+    for c in ctxs:
+        c.set_ignore(ign)
+    v = np.full((3, m), 0xFF, np.uint8)
+    last = 0
+    for batch in range(2):
+        t, oc = synth.sparse_np(n, m, seed=3122 + batch, hot_frac=0.05)
+        for j in (50, counts[0], counts[0] + counts[1] + 64):
+            _collide(t, j, zc, rng)             # inside, at shard 1's row 0, at a chunk start
+        _collide(t, counts[0] + 100, zc, rng)
+        t[counts[0] + 101:counts[0] + 140] = t[counts[0] + 100]  # a chain over a chunk boundary
+        exp = oracle.triage_batch(MODE_DYNAMORIO, t, oc, virgin=v, ignore=ign, last_hash=last,
+                                  want=oracle.WANT_H32)
+        lo, shards, ocs = 0, [], []
+        for c in counts:
+            shards.append(torch.from_numpy(t[lo:lo + c].copy()).cuda())
+            ocs.append(torch.from_numpy(oc[lo:lo + c].copy()).cuda())
+            lo += c
+        hnb, h32 = _run_shards(ctxs, shards, ocs, MODE_DYNAMORIO, torch.device("cuda"), fused)
+        np.testing.assert_array_equal(hnb, exp["hnb"])
+        np.testing.assert_array_equal(h32, exp["h32"])
+        for c in ctxs:
+            np.testing.assert_array_equal(c.get_virgin(), exp["virgin"])
+            assert c.last_hash == exp["last_hash"]
+        v, last = exp["virgin"], exp["last_hash"]
 
 
 @pytest.mark.parametrize("commit", [False, True], ids=["submit-copies", "early-commits"])

@@ -30,6 +30,38 @@ def test_tail_handoffs_are_ordered(product_isa):
     assert counts["tickets"] == 2 and counts["inv"] == 2, counts
 
 
+def test_small_ticket_and_pass1_lookback(product_isa):
+    """Every other kernel with an in-launch hand-off: k_small's last-workgroup ticket (drain,
+    barrier, agent release waited for, returning atomic add; its sc1 dword stores re-arm words
+    for the next launch) and k_pass1s's look-back in the fused skip rule (one 64-bit agent-scope
+    word carrying tag and hash: a single sc1 dwordx2 store, polled by sc1 dwordx2 loads).  The
+    staged kernels (k_skip, k_chain, k_total, k_scan, k_resolve, k_pack) hand nothing over
+    inside a launch: their consumers are the next launches."""
+    import handoff_isa_check as H
+
+    funcs = H.split_functions(product_isa.split("\n"))
+    small = [k for k in funcs if "k_small" in k]
+    assert len(small) == 2, sorted(funcs)[:10]
+    for k in small:
+        issues, counts = H.check(funcs[k], tickets=True, flags=False)
+        assert not issues, (k, issues[:5])
+        assert counts["tickets"] == 1 and counts["wbl2"] == 1 and counts["inv"] == 1, counts
+    p1s_dr = [k for k in funcs if "k_pass1s" in k and "k_pass1sILi1E" in k]
+    assert len(p1s_dr) == 4, sorted(k for k in funcs if "k_pass1s" in k)
+    for k in p1s_dr:
+        pub, poll, other = H.lookback(funcs[k])
+        assert len(pub) == 1 and len(poll) >= 1 and not other, (k, pub, poll, other)
+    for k in funcs:  # the AFL-mode instantiations have no look-back at all
+        if "k_pass1s" in k and k not in p1s_dr:
+            assert H.lookback(funcs[k]) == ([], [], []), k
+    staged = [k for k in funcs if any(f"{n}" in k for n in ("k_skip", "k_chain", "k_total",
+                                                             "k_scan", "k_resolve", "k_pack"))]
+    assert len(staged) >= 6
+    for k in staged:
+        b = funcs[k]
+        assert not any(x.startswith("buffer_wbl2") or x.startswith("buffer_inv") for x in b), k
+
+
 def test_checker_catches_unordered_handoffs():
     import handoff_isa_check as H
 

@@ -52,3 +52,13 @@ def test_checker_catches_a_reused_destination():
             "s_waitcnt vmcnt(0)",
             "s_endpgm"]
     assert V.scan_function(body)
+
+
+def test_patprobe2_register_modes_are_hazard_free():
+    """tools/patprobe2.hip (the staging calibration probe) with register-safe waits: no
+    instruction touches a register whose asm load is in flight, in any instantiation -- round 5's
+    plain-wait build of probe<0,256,3,0> faulted on the GPU (tools/patprobe2_hazards.py)."""
+    import patprobe2_hazards as P
+
+    out = []
+    assert P.report(P.isa([]), "current", out) == 0, "\n".join(out)

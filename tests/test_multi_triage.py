@@ -27,6 +27,9 @@ def _sharded_batches(mode, devices):
                 cut = n // len(devices)  # a repeat across the first shard boundary (DynamoRIO skip)
                 t[cut] = t[cut - 1]
                 t[n // 2 + 1] = t[n // 2]
+                for j in (64, cut + 64, cut + 128):  # repeats at 64-row chunk starts inside a
+                    if j < n:                        # shard: the pass-1 look-back's row compare
+                        t[j] = t[j - 1]
             exp = oracle.triage_batch(mode, t, oc, virgin=v, last_hash=last, want=oracle.WANT_H32)
             got = mc.triage_host(t, oc, WANT_H32)
             np.testing.assert_array_equal(got["hnb"], exp["hnb"])
@@ -39,10 +42,14 @@ def _sharded_batches(mode, devices):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pass1", ["narrow", "wide"])
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("workers", [2, 3])
-def test_sharded_batches_from_c(gpu, mode, workers):
-    """Workers sharing cuda:0 (device-local copies)."""
+def test_sharded_batches_from_c(gpu, mode, workers, pass1, monkeypatch):
+    """Workers sharing cuda:0 (device-local copies).  Both pass-1 kernels: the shards here are a
+    few chunks, which AUTO sends to the wide kernels; narrow forces k_pass1s, whose epilogue runs
+    the skip rule (rows j >= 1 of a shard, with the look-back across its chunks)."""
+    monkeypatch.setenv("KBZ_PASS1", pass1)
     _sharded_batches(mode, [0] * workers)
 
 
@@ -55,6 +62,43 @@ def test_sharded_batches_from_c_distinct_gpus(gpu, mode):
     if torch.cuda.device_count() < 2:
         pytest.skip("needs >= 2 GPUs")
     _sharded_batches(mode, list(range(min(torch.cuda.device_count(), 4))))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", MODES)
+def test_sharded_resident_batches_from_c(gpu, mode):
+    """kbz_triage_batch_devices_resident: shards already on the devices (three workers sharing
+    cuda:0, one of them empty), two batches in a row with repeats at the shard boundaries, equal
+    to one sequential pass; then a host batch through the same context continues the state."""
+    import torch
+
+    m = 4096
+    v = np.full((3, m), 0xFF, np.uint8)
+    last = 0
+    with MultiTriageContext(m, mode, 512, devices=[0, 0, 0]) as mc:
+        assert mc.peer_pairs() == 0  # one distinct device: nothing to enable
+        for b, counts in enumerate([(300, 0, 211), (64, 129, 1)]):
+            n = sum(counts)
+            t, oc = synth.sparse_np(n, m, seed=900 + 7 * b + mode, hot_frac=0.05)
+            t[counts[0]] = t[counts[0] - 1] if counts[0] and n > counts[0] else t[counts[0]]
+            exp = oracle.triage_batch(mode, t, oc, virgin=v, last_hash=last, want=oracle.WANT_H32)
+            shards, ocs, lo = [], [], 0
+            for c in counts:
+                shards.append(torch.from_numpy(t[lo:lo + c].copy()).cuda())
+                ocs.append(torch.from_numpy(oc[lo:lo + c].copy()).cuda())
+                lo += c
+            got = mc.triage_resident(shards, ocs, WANT_H32)
+            hnb = np.concatenate([h.cpu().numpy() for h in got["hnb"]])
+            np.testing.assert_array_equal(hnb, exp["hnb"])
+            if mode == 1:
+                h32 = np.concatenate([h.cpu().numpy().view(np.uint32) for h in got["h32"]])
+                np.testing.assert_array_equal(h32, exp["h32"])
+                assert mc.last_hash == exp["last_hash"]
+            np.testing.assert_array_equal(mc.get_virgin(), exp["virgin"])
+            v, last = exp["virgin"], exp.get("last_hash", last)
+        t, oc = synth.sparse_np(400, m, seed=950 + mode, hot_frac=0.05)
+        exp = oracle.triage_batch(mode, t, oc, virgin=v, last_hash=last, want=oracle.WANT_H32)
+        np.testing.assert_array_equal(mc.triage_host(t, oc, WANT_H32)["hnb"], exp["hnb"])
 
 
 @pytest.mark.gpu

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Static check of the in-launch hand-offs of the fused tail (k_tail, k_fin) on the compiled ISA.
+"""Static check of the in-launch hand-offs (k_tail, k_fin, k_small's ticket, k_pass1s's look-back
+word) on the compiled ISA.
 
 The hand-offs follow MI355X_MICROARCH.md's valid forms (§ inter-workgroup visibility):
   * producer with plain payload stores: every storing wave `s_waitcnt vmcnt(0)`, `s_barrier`,
@@ -45,11 +46,15 @@ def drains(ins):
     return ins.startswith("s_waitcnt") and re.search(r"vmcnt\(0\)", ins) is not None
 
 
-def check(body, tickets=True):
+def check(body, tickets=True, flags=True):
     """Returns (issues, counts) for one kernel body; tickets=False: returning atomic adds are
-    list reservations (k_tail's item / fix-list appends), not signals."""
+    list reservations (k_tail's item / fix-list appends), not signals; flags=False: the kernel's
+    `sc1` dword stores re-arm words for the next launch (k_small), they signal nothing in-launch.
+    A `buffer_wbl2` (release) waited for by `s_waitcnt vmcnt(0)` after the workgroup barrier
+    keeps that barrier valid for a following ticket (k_small: drain, barrier, release, ticket)."""
     issues = []
     pending = False        # a VMEM write may be in flight
+    payload = False        # ... of which a store / atomic (not only a release)
     barrier_after_drain = False
     wbl2_open = None       # index of a buffer_wbl2 not yet followed by vmcnt(0)
     inv_open = None        # index of a buffer_inv sc1 not yet followed by vmcnt(0)
@@ -57,9 +62,10 @@ def check(body, tickets=True):
     for i, ins in enumerate(body):
         op = ins.split()[0]
         if drains(ins):
-            if pending:  # writes were in flight: a barrier must follow this drain
+            if payload:  # stores / atomics were in flight: a barrier must follow this drain
                 barrier_after_drain = False
             pending = False
+            payload = False
             wbl2_open = None
             inv_open = None
             continue
@@ -83,7 +89,7 @@ def check(body, tickets=True):
             if wbl2_open is not None:
                 issues.append((wbl2_open, body[wbl2_open], f"release not waited before {ins}"))
                 wbl2_open = None
-            is_flag = op == "global_store_dword" and re.search(r"\bsc1\b", ins)
+            is_flag = flags and op == "global_store_dword" and re.search(r"\bsc1\b", ins)
             is_ticket = tickets and op == "global_atomic_add" and re.search(r"\bsc0\b", ins)
             if is_flag:
                 counts["flag_stores"] += 1
@@ -95,8 +101,21 @@ def check(body, tickets=True):
                     issues.append((i, ins, "ticket without drain + barrier"))
             if op.startswith(WRITE):
                 pending = True
+                payload = True
                 barrier_after_drain = False
     return issues, counts
+
+
+def lookback(body):
+    """k_pass1s's in-launch look-back (the fused skip rule): the previous chunk's last-row hash
+    travels with the batch tag in ONE 64-bit agent-scope word -- published by one
+    `global_store_dwordx2 ... sc1`, polled by `global_load_dwordx2 ... sc1` -- so there is no
+    payload to order it after.  Returns (publishes, polls, other sc1 stores)."""
+    pub = [x for x in body if x.startswith("global_store_dwordx2") and re.search(r"\bsc1\b", x)]
+    poll = [x for x in body if x.startswith("global_load_dwordx2") and re.search(r"\bsc1\b", x)]
+    other = [x for x in body if x.startswith(("global_store", "buffer_store")) and
+             re.search(r"\bsc1\b", x) and x not in pub]
+    return pub, poll, other
 
 
 def main():

@@ -19,6 +19,34 @@ template <int N>
 __device__ __forceinline__ void vmwait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// The register modes' counted wait names the slot's registers "+v" (as k_pass1s's
+// vmcnt_wait_ring does): the compiler can neither read them above the wait nor hand them to
+// another value while their loads are in flight.  Round 5's probe used the plain wait above:
+// in probe<0,256,3,0> the compiler hoisted the ORs of slot 1 above the wait, took v[0:3] (slot
+// 1's first row, still in flight) as free and computed the next load's address into v[0:1]; the
+// load landed on it, and the next global_load_dwordx4 v[0:3], v[0:1] read address
+// 0x0101010101010101 (the 0x01 fill): HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION
+// (tools/patprobe2_hazards.py, profiles/r06/patprobe2_fault.txt).
+template <int N>
+__device__ __forceinline__ void vmwait_slot(u32x4 (&r)[4]) {
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]) : "n"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vmwait_slot(u32x4 (&r)[5]) {
+  asm volatile("s_waitcnt vmcnt(%5)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]) : "n"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vmwait_slot(u32x4 (&r)[8]) {
+  asm volatile("s_waitcnt vmcnt(%8)"
+               : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7])
+               : "n"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vmwait_slot(u32x4 (&r)[9]) {
+  asm volatile("s_waitcnt vmcnt(%9)"
+               : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]), "+v"(r[8])
+               : "n"(N) : "memory");
+}
 __device__ __forceinline__ void raw_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
@@ -73,7 +101,11 @@ __global__ __launch_bounds__(128) void probe(const unsigned char *base, size_t M
 #pragma unroll
       for (int d = 0; d < D; d++) {
         const int t = t0 + d;
+#ifdef PATPROBE2_PLAIN_WAIT  // round 5's wait: compiled for tools/patprobe2_hazards.py only
         vmwait<(D - 1) * (NLD + NV)>();
+#else
+        vmwait_slot<(D - 1) * (NLD + NV)>(r[d]);
+#endif
         if (MODE == 0) {
 #pragma unroll
           for (int i = 0; i < NLD; i++) acc |= r[d][i];
@@ -157,10 +189,12 @@ int main() {
   if (hipMalloc(&p, n * S) != hipSuccess || hipMalloc(&o, 4) != hipSuccess) return 1;
   (void)hipMemset(p, 1, n * S);
   (void)hipDeviceSynchronize();
-  // register modes only at D = 2: deeper rings here lack k_pass1s's register-safe waits
-  // (tools/vmem_hazard_cfg.py flags them) and one faulted on the GPU (profiles/r05/patprobe2.txt)
+  // every configuration passes tools/vmem_hazard_cfg.py (tools/patprobe2_hazards.py checks the
+  // ISA before the probe is run); round 5's probe<0,256,3,0>, which faulted, is the third line
   run<0, 256, 2, 0>(p, n, M, S, o);
   run<1, 256, 2, 0>(p, n, M, S, o);
+  run<0, 256, 3, 0>(p, n, M, S, o);
+  run<1, 256, 3, 0>(p, n, M, S, o);
   run<3, 256, 2, 0>(p, n, M, S, o);
   run<2, 256, 0, 4>(p, n, M, S, o);
   run<2, 128, 0, 4>(p, n, M, S, o);

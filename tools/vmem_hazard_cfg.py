@@ -112,6 +112,13 @@ def step(q, t, issues=None, where=None):
             q = q[: int(m.group(1))]
         return q
     pend = set().union(*q) if q else set()
+    if op.startswith(VMEM_LOAD) and ("_lds_" in op or " lds" in t):
+        # LDS-DMA (global_load_lds_dwordx4 vaddr, ...): no VGPR destination, the data goes to
+        # LDS at M0; every VGPR operand is an address source
+        srcs = set().union(*[regs(o) for o in ops]) if ops else set()
+        if issues is not None and srcs & pend:
+            issues.append((where, t, "address reads pending", sorted(srcs & pend)))
+        return ([set()] + q)[:QMAX]
     if op.startswith(VMEM_LOAD):
         srcs = set().union(*[regs(o) for o in ops[1:]]) if len(ops) > 1 else set()
         if issues is not None and srcs & pend:
