@@ -1621,7 +1621,8 @@ __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
       // m is complete here, so no value of the slot is still live when its registers are
       // reloaded (otherwise the compiler renames the slot and copies it while loads fly)
       asm volatile("" : "+v"(m));
-      load(R[u], t + D);  // the ring slot is free again
+      // the tile's writes before the slot's next loads (as in k_pass1d: written after them, the
+      // next step's load-counting wait also waited for the tile just prefetched)
       if (s0 + u < t1 - t0) {
         const bool any = (m.x | m.y | m.z | m.w) != 0;
         const uint64_t bal = __ballot(any);
@@ -1651,6 +1652,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_pass1n(Pass1Args a) {
           for (int k = 0; k < NC; k++) tfl[k] = 0;
         }
       }
+      load(R[u], t + D);  // the ring slot is free again
     }
   }
   drain_asm_loads(R);
@@ -1902,6 +1904,9 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
       for (int u = 0; u < D; u++) {
         const uint32_t q = q0 + u;
         const uint32_t t = tile_of(q);
+        // younger than slot u's loads: the next D - 1 tiles' loads and the VMEM writes issued
+        // before each of them (counted as loads here: the wait also covers those writes, which
+        // were issued a step or more ago -- see the writes below)
         vmcnt_wait_ring<(D - 1) * NR>(R[u]);
         KBZ_STAMP(0);
         // classify_counts in place, the column OR (rows past the end of a partial chunk are
@@ -1957,7 +1962,12 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
           asm volatile("" ::: "memory");
           if (lane == 0) KBZ_FST(ready, sl, (int)t);
         }
-        load(R[u], q + D);  // the ring slot is free again
+        // The tile's writes (chunk_or, segment-OR atomics: still-virgin bits only) go BEFORE the
+        // slot's next loads.  vmcnt counts loads and writes in issue order: written after the
+        // loads, the next step's wait -- which counts only loads -- also waited for the oldest
+        // loads of the tile just prefetched, a memory latency per step whenever tiles are stored
+        // (novelty-heavy batches: every tile).  Written before them, that wait covers writes
+        // issued a step earlier.
         if (mine) {
           const bool any = (m.x | m.y | m.z | m.w) != 0;
           if (__ballot(any)) {
@@ -1975,6 +1985,7 @@ __global__ __launch_bounds__(64 * (NX / 3 * 4), 1) void k_pass1d(Pass1Args a) {
             if (hi) atomicOr(sp + 1, (unsigned long long)hi);
           }
         }
+        load(R[u], q + D);  // the ring slot is free again
         KBZ_STAMP(3);
       }
     }
@@ -3238,6 +3249,9 @@ struct FinArgs {
   const uint32_t *fix_cnt;  // null: AFL modes (no fix list)
   uint32_t nchunks;
 };
+#ifndef KBZ_FIN_GRID  // k_fin's workgroups (its waves share out the claim items)
+#define KBZ_FIN_GRID 512
+#endif
 constexpr uint32_t kFinCopiers = 16;
 __device__ __forceinline__ bool spin_until_ge(const uint32_t *p, uint32_t want) {
   for (uint32_t it = 0; it < kSpinMax; it++) {
@@ -4605,7 +4619,7 @@ int fused_tail(kbz_ctx *c, uint8_t *hnb_out, hipStream_t s) {
   f.fix_cnt = dr ? c->counters + 3 : nullptr;
   f.nchunks = c->cur_chunks;
   if (stage_begin(c, s, &st0)) return -1;
-  hipLaunchKernelGGL(k_fin, dim3(512), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(k_fin, dim3(KBZ_FIN_GRID), dim3(256), 0, s, f);
   HIP_TRY(hipGetLastError());
   if (stage_end(c, s, KBZ_STAGE_RESOLVE, st0)) return -1;
   std::swap(c->segor, c->segor_alt);
@@ -4929,7 +4943,7 @@ int kbz_shard_finish_gathered(kbz_ctx_t *c, const uint8_t *d_gathered, size_t ra
   f.fix_cnt = dr ? c->counters + 3 : nullptr;
   f.nchunks = c->cur_chunks;
   if (stage_begin(c, s, &st0)) return -1;
-  hipLaunchKernelGGL(k_fin, dim3(512), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(k_fin, dim3(KBZ_FIN_GRID), dim3(256), 0, s, f);
   HIP_TRY(hipGetLastError());
   if (stage_end(c, s, KBZ_STAGE_RESOLVE, st0)) return -1;
   std::swap(c->segor, c->segor_alt);

@@ -62,12 +62,16 @@ if [ -n "$TAILST" ]; then
   KBZ_TAIL_NOVELTY=${TAILST_NOVELTY:-0} KBZ_TAIL_BATCHES=${TAILST_BATCHES:-16} KBZ_HIP_LIB=$PWD/build_variants/tailst/libkbz_hip.so timeout -k 10 300 python tools/tail_stamps.py > $O/tail_stamps.txt 2>&1 || { tail $O/tail_stamps.txt; exit 1; }
   tail -4 $O/tail_stamps.txt
 fi
-if [ -n "$NOVTRACE" ]; then
-  step noveltytrace
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_nov -o run -- python3 tools/novelty_trace.py 5 > $O/novelty_trace.json 2> $O/novelty_trace.err || { tail $O/novelty_trace.err; exit 1; }
-  python3 scripts/ktrace_kernels.py $O/prof_nov > $O/novelty_kernels.json || exit 1
-  rm -f $(find $O/prof_nov -name '*kernel_trace.csv')
-  cat $O/novelty_trace.json; tail -c 600 $O/novelty_kernels.json; echo
+if [ -n "$NOVTRACE" ]; then  # NOVTRACE="name|STEPS MODE WORKLOAD;..." (tools/novelty_trace.py)
+  IFS=';' read -ra L <<< "$NOVTRACE"
+  for leg in "${L[@]}"; do
+    name=${leg%%|*}; args=${leg#*|}
+    step "noveltytrace $name ($args)"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_nov_$name -o run -- python3 tools/novelty_trace.py $args > $O/novelty_trace_$name.json 2> $O/novelty_trace_$name.err || { tail $O/novelty_trace_$name.err; exit 1; }
+    python3 scripts/ktrace_kernels.py $O/prof_nov_$name > $O/novelty_kernels_$name.json || exit 1
+    rm -f $(find $O/prof_nov_$name -name '*kernel_trace.csv')
+    cat $O/novelty_trace_$name.json
+  done
 fi
 if [ -n "$PROBE" ]; then
   step l2probe
