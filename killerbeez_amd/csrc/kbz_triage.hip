@@ -3420,6 +3420,10 @@ __global__ __launch_bounds__(256) void k_fin(FinArgs a) {
 // at a time (from pinned host memory on the plugin's zero-copy path).
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t kSmallRows = 64;
+#ifndef KBZ_SMALL_TPB  // k_small's threads per workgroup (64: one wave each, 4x the workgroups)
+#define KBZ_SMALL_TPB 256
+#endif
+static_assert(KBZ_SMALL_TPB >= (int)kSmallRows && KBZ_SMALL_TPB % 64 == 0, "k_small block");
 struct SmallArgs {
   const uint8_t *traces;
   size_t stride;
@@ -3438,7 +3442,7 @@ __device__ __forceinline__ uint4 xform16(uint4 a, int xf) {
   return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 template <int MODE>
-__global__ __launch_bounds__(256) void k_small(SmallArgs a) {
+__global__ __launch_bounds__(KBZ_SMALL_TPB) void k_small(SmallArgs a) {
   static_assert(MODE != KBZ_MODE_DYNAMORIO, "DynamoRIO hashes every trace (k_pass1*)");
   __shared__ uint32_t score[kSmallRows];
   __shared__ int last;
@@ -4966,11 +4970,12 @@ int kbz_triage_batch_device(kbz_ctx_t *c, const uint8_t *traces, size_t n, size_
     const int vn = c->vcur ^ 1;
     SmallArgs a{traces, stride, (uint32_t)n, (uint32_t)c->M, outcome, c->V[c->vcur], c->V[vn],
                 c->hnb32, hnb_out, c->counters + 12, c->counters + 8};
-    const dim3 grid(cdiv(c->M / 16, 256));
+    const dim3 grid(cdiv(c->M / 16, KBZ_SMALL_TPB));
     if (c->mode == KBZ_MODE_AFL)
-      hipLaunchKernelGGL(k_small<KBZ_MODE_AFL>, grid, dim3(256), 0, (hipStream_t)stream, a);
+      hipLaunchKernelGGL(k_small<KBZ_MODE_AFL>, grid, dim3(KBZ_SMALL_TPB), 0, (hipStream_t)stream, a);
     else
-      hipLaunchKernelGGL(k_small<KBZ_MODE_AFL_CLASSIFY>, grid, dim3(256), 0, (hipStream_t)stream, a);
+      hipLaunchKernelGGL(k_small<KBZ_MODE_AFL_CLASSIFY>, grid, dim3(KBZ_SMALL_TPB), 0,
+                         (hipStream_t)stream, a);
     HIP_TRY(hipGetLastError());
     c->vcur = vn;
     return 0;

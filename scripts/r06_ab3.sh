@@ -17,3 +17,7 @@ echo "== novelty afl $(date +%T)"
 VARIANTS="base wbefore base_2 wbefore_2" NOV_ARGS="5 afl config2" timeout -k 10 600 bash scripts/ab_novelty_trace.sh > $O/ab_novelty_afl.txt 2>&1; rc=$?; cat $O/ab_novelty_afl.txt; [ $rc -eq 0 ] || exit 1
 echo "== fresh config3 $(date +%T)"
 STEPS=6 VARIANTS="base wbefore base_2 wbefore_2" BENCH_ARGS="--workload config3" timeout -k 10 900 bash scripts/ab_variants.sh > $O/ab_config3.txt 2>&1; rc=$?; cat $O/ab_config3.txt; [ $rc -eq 0 ] || exit 1
+echo "== T late prefetch, fresh config2 $(date +%T)"
+STEPS=10 VARIANTS="base tlate tlate3 base_2 tlate_2 tlate3_2" timeout -k 10 900 bash scripts/ab_variants.sh > $O/ab_tlate_config2.txt 2>&1; rc=$?; cat $O/ab_tlate_config2.txt; [ $rc -eq 0 ] || exit 1
+echo "== T late prefetch, novelty config2 $(date +%T)"
+VARIANTS="base tlate tlate3 base_2 tlate_2" NOV_ARGS="5 dynamorio config2" timeout -k 10 900 bash scripts/ab_novelty_trace.sh > $O/ab_tlate_novelty_c2.txt 2>&1; rc=$?; cat $O/ab_tlate_novelty_c2.txt; [ $rc -eq 0 ] || exit 1
