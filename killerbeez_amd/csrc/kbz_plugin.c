@@ -97,6 +97,9 @@ typedef struct kbz_plugin {
   uint8_t *r_hnb;          /* results of the last flushed window */
   size_t r_n;
   long r_base;
+  uint8_t *w_hnb;          /* results of the window being recorded (its submitted parts) */
+  size_t q_off;            /* execs of this window already submitted as sub-batches */
+  size_t sub_k;            /* afl_gpu: submit every sub_k execs of a small window (0: off) */
   long last_ticket;        /* -1 until the first record */
   int last_fuzz_result;
   int last_path_was_new;   /* has_new_coverage result of the last triaged exec (DR state key) */
@@ -426,6 +429,7 @@ static void plugin_free(kbz_plugin_t *p) {
   free(p->ignore);
   free(p->virgin);
   free(p->r_hnb);
+  free(p->w_hnb);
   free(p);
 }
 
@@ -470,7 +474,11 @@ static kbz_plugin_t *plugin_alloc(int mode, size_t map_size, size_t max_batch) {
   p->early_copy = !ec || atoi(ec) != 0;
   p->virgin = (uint8_t *)malloc(3 * map_size);
   p->r_hnb = (uint8_t *)malloc(max_batch);
-  if (!p->virgin || !p->r_hnb) {
+  p->w_hnb = (uint8_t *)malloc(max_batch);
+  const char *sk = getenv("KBZ_PLUGIN_SUBBATCH");
+  p->sub_k = sk ? (size_t)strtoul(sk, NULL, 0) : 0;
+  if (p->sub_k > 64) p->sub_k = 64;  /* a sub-batch is read from the pinned slot (<= 64 rows) */
+  if (!p->virgin || !p->r_hnb || !p->w_hnb) {
     plugin_free(p);
     set_err("out of host memory");
     return NULL;
@@ -835,13 +843,15 @@ static int dr_first_enable(kbz_plugin_t *p) {
 /* Triage the queued execs (the acquired ring slot) as one ordered batch and wait for it.  A
  * batch of at most 64 execs is read by the GPU straight from the pinned slot (no DMA). */
 static int plugin_flush(kbz_plugin_t *p) {
-  if (!p->q_rows) return 0;
+  if (!p->q_rows && !p->q_off) return 0;
   slot_copies_done();
   p->mirror_stale = 1;
-  const size_t n = p->q_n;
+  const size_t n = p->q_off + p->q_n;  /* the window: submitted sub-batches + the slot's rows */
+  const size_t nq = p->q_n, off = p->q_off;
   const uint8_t *rows = p->q_rows;  /* the slot stays valid until the next record */
   p->q_rows = NULL;
   p->q_n = 0;
+  p->q_off = 0;
   if (p->per_module) {  /* has_new_coverage_per_module over the batch */
     size_t offs[p->nmod];
     for (size_t i = 0; i < p->nmod; i++) offs[i] = i * p->map_size;
@@ -851,18 +861,27 @@ static int plugin_flush(kbz_plugin_t *p) {
       return -1;
     }
     for (size_t i = 0; i < p->nmod; i++) p->mnew[i] = p->r_mhnb[i * n + n - 1] != 0;
-  } else if (kbz_ring_submit(p->ctx, n, 1, p->r_hnb, p->dump_dir ? p->r_h32 : NULL, NULL,
-                             p->dump_dir ? KBZ_WANT_H32 : 0) ||
-             kbz_ring_flush(p->ctx)) {
-    set_err("GPU triage: %s", kbz_last_error());
-    return -1;
+  } else {
+    /* the slot's rows (after any sub-batches: AFL, no hashes), results into the window's buffer;
+     * the flush delivers every part, then the window's buffer becomes the queryable one */
+    if ((nq && kbz_ring_submit(p->ctx, nq, 1, p->w_hnb + off,
+                               p->dump_dir ? p->r_h32 + off : NULL, NULL,
+                               p->dump_dir ? KBZ_WANT_H32 : 0)) ||
+        kbz_ring_flush(p->ctx)) {
+      set_err("GPU triage: %s", kbz_last_error());
+      return -1;
+    }
+    uint8_t *t = p->r_hnb;
+    p->r_hnb = p->w_hnb;
+    p->w_hnb = t;
   }
   /* the window's results and tickets first: the side outputs below cannot undo them */
   p->last_path_was_new = p->r_hnb[n - 1] != 0;
   p->r_base = p->q_base;
   p->r_n = n;
   p->q_base += (long)n;
-  plugin_window_done(p, rows, n, (p->per_module ? p->nmod : 1) * p->map_size);
+  /* (sub-batched windows are AFL windows: plugin_window_done reads no rows for them) */
+  plugin_window_done(p, off ? NULL : rows, n, (p->per_module ? p->nmod : 1) * p->map_size);
   return 0;
 }
 
@@ -876,7 +895,8 @@ static long plugin_record(kbz_plugin_t *p, const uint8_t *trace, int fuzz_result
     set_err("fuzz_result must be FUZZ_NONE, FUZZ_HANG or FUZZ_CRASH");
     return -1;
   }
-  if (p->q_rows && p->q_n == p->q_cap && plugin_flush(p)) return -1;
+  if (((p->q_rows && p->q_n == p->q_cap) || p->q_off == p->max_batch) && plugin_flush(p))
+    return -1;
   if (dr_first_enable(p)) return -1;
   if (p->per_module && !p->q_rows) {  /* module maps back to back: nmod * map_size bytes */
     if (ensure_ctx(p)) return -1;
@@ -891,14 +911,29 @@ static long plugin_record(kbz_plugin_t *p, const uint8_t *trace, int fuzz_result
       set_err("GPU ring: %s", kbz_last_error());
       return -1;
     }
-    if (p->q_cap > p->max_batch) p->q_cap = p->max_batch;
+    if (p->q_cap > p->max_batch - p->q_off) p->q_cap = p->max_batch - p->q_off;
   }
   const size_t row = (p->per_module ? p->nmod : 1) * p->map_size;
   copy_to_slot(p->q_rows + p->q_n * row, trace, row);
   /* the KBZ_FUZZ_* outcomes of kbz_triage.h use the same numbering */
   p->q_outcome[p->q_n] = (int8_t)fuzz_result;
-  p->last_ticket = p->q_base + (long)p->q_n++;
+  p->last_ticket = p->q_base + (long)(p->q_off + p->q_n++);
   p->last_fuzz_result = fuzz_result;
+  /* afl_gpu, small windows: every sub_k execs the slot's rows go to the GPU as their own batch
+   * (one k_small launch reading them from the pinned slot) while the next execs are recorded in
+   * the other slot; the result query then waits for the last part only */
+  if (p->sub_k && p->q_n == p->sub_k && p->q_off + p->q_n <= 64 && p->mode == KBZ_MODE_AFL &&
+      !p->per_module && !p->dump_dir) {
+    slot_copies_done();
+    if (kbz_ring_submit(p->ctx, p->q_n, 1, p->w_hnb + p->q_off, NULL, NULL, 0)) {
+      set_err("GPU triage: %s", kbz_last_error());
+      return -1;
+    }
+    p->q_off += p->q_n;
+    p->q_n = 0;
+    p->q_rows = NULL;
+    return p->last_ticket;
+  }
   /* every 64 execs past the first 128 (a window that will not fit the pinned-read path of
    * <= 64 rows): the rows recorded so far start their copy to the GPU now, overlapped with the
    * execs still to come, instead of all at the result query.  The copy is only started early;

@@ -224,6 +224,34 @@ def test_deferred_windows_with_early_copies(gpu, name, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sub_k", [1, 4, 8])
+def test_afl_sub_batched_windows(gpu, monkeypatch, sub_k):
+    """afl_gpu with KBZ_PLUGIN_SUBBATCH: small windows go to the GPU in parts of sub_k execs
+    while recording continues (alternating ring slots); windows of 1, 3, sub_k, sub_k + 1, 16,
+    70 (sub-batches up to 64 rows, then one part) and 200 (early commits in its last part), plus
+    a query of an older ticket of the window and of the window before, equal the per-exec
+    results."""
+    monkeypatch.setenv("KBZ_PLUGIN_SUBBATCH", str(sub_k))
+    wins = [1, 3, sub_k, sub_k + 1, 16, 70, 200]
+    n = sum(wins)
+    t, oc = synth.sparse_np(n, M, seed=31 + sub_k, hot_frac=0.05, outcome_p=(0.8, 0.1, 0.1))
+    exp = _expected(oracle.MODE_AFL, t, oc)
+    p = P.Plugin("afl_gpu", f'{{"map_size": {M}, "max_batch": 256}}')
+    got, lo = [], 0
+    for w in wins:
+        tickets = [p.record(t[j], int(oc[j])) for j in range(lo, lo + w)]
+        assert tickets == list(range(lo, lo + w))
+        got += [p.result(k) for k in tickets]
+        assert p.result(tickets[0]) == exp["hnb"][lo]  # an older ticket of this window
+        lo += w
+    np.testing.assert_array_equal(np.array(got, np.uint8), exp["hnb"])
+    maps = P.state_maps(p.get_state(), M)
+    np.testing.assert_array_equal(maps["virgin_bits"], exp["virgin"][0])
+    np.testing.assert_array_equal(maps["virgin_tmout"], exp["virgin"][1])
+    np.testing.assert_array_equal(maps["virgin_crash"], exp["virgin"][2])
+
+
+@pytest.mark.gpu
 def test_dynamorio_ignore_file(gpu, tmp_path):
     rng = np.random.default_rng(4)
     ign = np.where(rng.random(M) < 0.4, 0, rng.integers(1, 256, M)).astype(np.uint8)
