@@ -2377,6 +2377,9 @@ __device__ __forceinline__ void flush_items(ItemStage &st, uint64_t *items, uint
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the area is reused
   st.n = 0;
 }
+#ifndef KBZ_WIN_LANEMASK  // window items: lanes without new bits load none of the window's rows
+#define KBZ_WIN_LANEMASK 1
+#endif
 #ifndef KBZ_WIN_ITEMS  // claimed bytes of one chunk's 1-KiB column window from which k_resolve
 #define KBZ_WIN_ITEMS 16  // streams the window's 64 rows (64 KiB, coalesced) instead of reading
 #endif                    // one scattered byte per row and claimed byte
@@ -2398,8 +2401,12 @@ __device__ __forceinline__ void emit_items_wave(uint32_t chunk, int k, uint32_t 
     // OR before this chunk replaces the chunk's (consumed) column OR in chunk_or, and k_resolve
     // re-derives the claims row by row in order: new bits of row r = t_r & V & ~(prev | rows < r)
     if (live) {  // read by whichever wave resolves the item (maybe another workgroup)
-      st_sc1((uint64_t *)win_prev, (uint64_t)prev.x | ((uint64_t)prev.y << 32));
-      st_sc1((uint64_t *)win_prev + 1, (uint64_t)prev.z | ((uint64_t)prev.w << 32));
+      // a lane whose 16 B hold no new bit gets prev = all ones: no row can claim there, and the
+      // resolver loads nothing for it (KBZ_WIN_LANEMASK; dense novelty-heavy windows have
+      // claims in a fraction of their lanes)
+      const bool none = KBZ_WIN_LANEMASK && (nb.x | nb.y | nb.z | nb.w) == 0;
+      st_sc1((uint64_t *)win_prev, none ? ~0ull : (uint64_t)prev.x | ((uint64_t)prev.y << 32));
+      st_sc1((uint64_t *)win_prev + 1, none ? ~0ull : (uint64_t)prev.z | ((uint64_t)prev.w << 32));
     }
     const uint32_t wcol = __shfl(col, 0);
     if (st.n + 1 > kWaveItems) flush_items(st, items, cap, counters);
@@ -2723,6 +2730,8 @@ __device__ __forceinline__ void resolve_window(const ResolveArgs &r, uint32_t ch
   uint64_t vr0 = ((uint64_t)vir.x | ((uint64_t)vir.y << 32)) & rel0;
   uint64_t vr1 = ((uint64_t)vir.z | ((uint64_t)vir.w << 32)) & rel1;
   if (!live) vr0 = vr1 = 0;
+  // the emitter marked lanes without new bits with an all-ones prev: they read no rows
+  const bool act = live && !(KBZ_WIN_LANEMASK && pa0 == ~0ull && pa1 == ~0ull);
   // bytes with V == 0xff (examined): a 2 is possible there while prev | acc is still 0
   const uint64_t ff0 = ~nonzero_bytes8(~vr0), ff1 = ~nonzero_bytes8(~vr1);
   const int xf = class_xf(r.mode, k);
@@ -2736,7 +2745,7 @@ __device__ __forceinline__ void resolve_window(const ResolveArgs &r, uint32_t ch
       rr[u] = rows ? __builtin_ctzll(rows) : -1;
       rows &= rows - 1;
       const uint64_t rw = row0 + (rr[u] >= 0 ? rr[u] : 0);
-      v[u] = *(const uint4 *)(r.traces + rw * r.stride + cl);
+      v[u] = act ? *(const uint4 *)(r.traces + rw * r.stride + cl) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < WR; u++) {

@@ -3,7 +3,7 @@
 # workgroups (small64) and sub-batched windows (KBZ_PLUGIN_SUBBATCH), alternating with the
 # product; then the plugin parity tests.
 cd "${GRAFT_REPO_ROOT}" || exit 1
-O=gpurun_out/r06_ab5; mkdir -p $O
+O=gpurun_out/${TAG:-r06_ab5}; mkdir -p $O
 echo "== pytest $(date +%T)"
 timeout -k 10 300 python -u -m pytest tests/test_plugin.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
 tail -1 $O/pytest.txt

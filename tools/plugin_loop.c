@@ -126,9 +126,9 @@ int main(int argc, char **argv) {
     }
     const double per = (now_s() - t0) / n;
     /* base: the host's own per-exec work (clear + the target's writes), no plugin calls; timed
-     * right after, twice, the faster kept (DRAM and page-cache state drift between runs) */
+     * right after, three times, the fastest kept (the pool's DRAM state drifts) */
     double base = 1e9;
-    for (int rep = 0; rep < 2; rep++) {
+    for (int rep = 0; rep < 3; rep++) {
       t0 = now_s();
       for (long e = 0; e < n; e++) {
         memset(map, 0, M);
