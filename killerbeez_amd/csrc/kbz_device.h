@@ -68,11 +68,15 @@ KBZ_HD uint64_t simplify8(uint64_t x) {
   return (uint64_t)simplify4((uint32_t)x) | ((uint64_t)simplify4((uint32_t)(x >> 32)) << 32);
 }
 
-// 0xff in every byte of x that is nonzero.
+// 0x80 in every byte of x that is nonzero, 0 elsewhere.
+KBZ_HD uint64_t nonzero_hi8(uint64_t x) {
+  return (((x & 0x7F7F7F7F7F7F7F7FULL) + 0x7F7F7F7F7F7F7F7FULL) | x) & 0x8080808080808080ULL;
+}
+// 0xff in every byte of x that is nonzero (0x80 - 0x01 = 0x7f borrows from no other byte; no
+// multiply: a 32-bit v_mul_lo_u32 is a quarter-rate instruction).
 KBZ_HD uint64_t nonzero_bytes8(uint64_t x) {
-  const uint64_t nz = (((x & 0x7F7F7F7F7F7F7F7FULL) + 0x7F7F7F7F7F7F7F7FULL) | x) &
-                      0x8080808080808080ULL;
-  return (nz >> 7) * 0xFFull;
+  const uint64_t nz = nonzero_hi8(x);
+  return nz | (nz - (nz >> 7));
 }
 
 // hash32 pieces (afl_progs/hash.h:36-65): per-word mix, chain step, finalizer.

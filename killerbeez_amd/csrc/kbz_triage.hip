@@ -257,6 +257,7 @@ __device__ __forceinline__ unsigned long long rt_now() {
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
   return t;
 }
+constexpr uint32_t kFinStampBase = kTailRecs / 2;  // k_fin's records (k_tail's below)
 #define KBZ_TAIL_DECL unsigned long long tl_t0 = rt_now(), tl_t1 = 0, tl_last = 0, tl_ph[4] = {0, 0, 0, 0}; uint32_t tl_walk = 0, tl_claims = 0, tl_flush = 0, tl_win = 0
 #define KBZ_TAIL_MARK() (tl_t1 = tl_last = rt_now())
 #define KBZ_TAIL_ADD(f, v) (tl_##f += (v))
@@ -268,6 +269,7 @@ __device__ __forceinline__ unsigned long long rt_now() {
     _r[2] = _e; _r[3] = ((unsigned long long)tl_walk << 48) | ((unsigned long long)(tl_claims & 0xffff) << 32) | ((tl_flush & 0xffff) << 16) | (tl_win & 0xffff); \
     for (int _p = 0; _p < 4; _p++) _r[4 + _p] = tl_ph[_p]; } } while (0)
 #else
+constexpr uint32_t kFinStampBase = 0;
 #define KBZ_TAIL_DECL do {} while (0)
 #define KBZ_TAIL_MARK() do {} while (0)
 #define KBZ_TAIL_ADD(f, v) do {} while (0)
@@ -2705,8 +2707,18 @@ struct ResolveArgs {  // what resolving a claim item needs (k_resolve, the fused
   const uint8_t *vcur;
   const uint8_t *ignore;
 };
-__device__ __forceinline__ void resolve_window(const ResolveArgs &r, uint32_t chunk, int k,
-                                               uint32_t wcol, const uint8_t *win_prev) {
+#ifndef KBZ_SCORE_SKIP  // window / byte items read the rows' scores so far and skip the atomicMax
+#define KBZ_SCORE_SKIP 1  // where it cannot raise one (exact: scores only grow until k_fin's copy).
+#endif                    // A novelty-heavy chunk has ~1,000 window items scoring the same 64 rows
+#ifndef KBZ_WIN_XF  // 1: the window loop instantiated per transform (no per-row branch; k_fin
+#define KBZ_WIN_XF 0  // 119 -> 181 VGPRs): config-3 novelty-heavy k_fin 0.599 vs 0.616 ms, AFL
+#endif                // 0.069 vs 0.048 ms (profiles/r06/ab/ab_winv_*.txt); 0: one loop, the
+                      // transform chosen per row at run time
+template <int XF>  // the class's transform (XF < 0: xf_rt, chosen at run time)
+__device__ __forceinline__ void resolve_window_xf(const ResolveArgs &r, uint32_t chunk, int k,
+                                                 uint32_t wcol, const uint8_t *win_prev,
+                                                 int xf_rt) {
+  const int xf = XF >= 0 ? XF : xf_rt;
   const int lane = threadIdx.x & 63;
   const uint64_t row0 = (uint64_t)chunk * kChunk;
   const uint64_t rl = row0 + lane;
@@ -2732,14 +2744,17 @@ __device__ __forceinline__ void resolve_window(const ResolveArgs &r, uint32_t ch
   if (!live) vr0 = vr1 = 0;
   // the emitter marked lanes without new bits with an all-ones prev: they read no rows
   const bool act = live && !(KBZ_WIN_LANEMASK && pa0 == ~0ull && pa1 == ~0ull);
-  // bytes with V == 0xff (examined): a 2 is possible there while prev | acc is still 0
-  const uint64_t ff0 = ~nonzero_bytes8(~vr0), ff1 = ~nonzero_bytes8(~vr1);
-  const int xf = class_xf(r.mode, k);
+  // bit 7 of each byte with V == 0xff (examined): a 2 is possible there while prev | acc is
+  // still 0
+  constexpr uint64_t kHi = 0x8080808080808080ull;
+  const uint64_t ff0 = ~nonzero_hi8(~vr0) & kHi, ff1 = ~nonzero_hi8(~vr1) & kHi;
   bool claimed = false;
   while (rows) {
     constexpr int WR = KBZ_WIN_ROWS;
     int rr[WR];
     uint4 v[WR];
+    // lane l: row l's score so far (refreshed every round trip, with the rows' loads)
+    const uint32_t have = (KBZ_SCORE_SKIP && rl < r.n) ? ld_sc1(&r.hnb32[rl]) : 0u;
 #pragma unroll
     for (int u = 0; u < WR; u++) {  // up to WR rows' loads in flight
       rr[u] = rows ? __builtin_ctzll(rows) : -1;
@@ -2753,18 +2768,27 @@ __device__ __forceinline__ void resolve_window(const ResolveArgs &r, uint32_t ch
       const uint64_t t0 = xform8((uint64_t)v[u].x | ((uint64_t)v[u].y << 32), xf) & rel0;
       const uint64_t t1 = xform8((uint64_t)v[u].z | ((uint64_t)v[u].w << 32), xf) & rel1;
       const bool nw = ((t0 & vr0 & ~pa0) | (t1 & vr1 & ~pa1)) != 0;
-      const bool two = ((nonzero_bytes8(t0) & ff0 & ~nonzero_bytes8(pa0)) |
-                        (nonzero_bytes8(t1) & ff1 & ~nonzero_bytes8(pa1))) != 0;
+      const bool two = ((nonzero_hi8(t0) & ff0 & ~nonzero_hi8(pa0)) |
+                        (nonzero_hi8(t1) & ff1 & ~nonzero_hi8(pa1))) != 0;
       pa0 |= t0;
       pa1 |= t1;
       const uint32_t sc = __ballot(two) ? 2u : __ballot(nw) ? 1u : 0u;
       if (sc) {
         claimed = true;
-        if (lane == 0) score_row(r.hnb32, row0 + rr[u], sc);
+        if (lane == 0 && __builtin_amdgcn_readlane(have, rr[u]) < sc)
+          score_row(r.hnb32, row0 + rr[u], sc);
       }
     }
   }
   if (!claimed && lane == 0) atomicOr(r.err, 8u);  // k_scan saw new bits here: inconsistent
+}
+__device__ __forceinline__ void resolve_window(const ResolveArgs &r, uint32_t chunk, int k,
+                                               uint32_t wcol, const uint8_t *win_prev) {
+  const int xf = class_xf(r.mode, k);  // wave-uniform
+  if (!KBZ_WIN_XF) resolve_window_xf<-1>(r, chunk, k, wcol, win_prev, xf);
+  else if (xf == XF_CLASSIFY) resolve_window_xf<XF_CLASSIFY>(r, chunk, k, wcol, win_prev, xf);
+  else if (xf == XF_SIMPLIFY) resolve_window_xf<XF_SIMPLIFY>(r, chunk, k, wcol, win_prev, xf);
+  else resolve_window_xf<XF_RAW>(r, chunk, k, wcol, win_prev, xf);
 }
 
 // One claim item (wave-uniform): a window item (new bits field 0) or one claimed byte of one
@@ -2787,6 +2811,7 @@ __device__ __forceinline__ void resolve_item(const ResolveArgs &r, uint64_t item
   const int oc = r.outcome ? r.outcome[rc] : KBZ_FUZZ_NONE;
   const uint8_t sk = r.skip ? r.skip[rc] : 0;
   const uint32_t raw = r.traces[rc * r.stride + col];
+  const uint32_t have = KBZ_SCORE_SKIP ? ld_sc1(&r.hnb32[rc]) : 0u;  // row rc's score so far
   const bool ok = row < r.n && class_of(r.mode, oc) == k && !sk;
   const uint32_t tb = ok ? byte_xform(raw, class_xf(r.mode, k)) : 0u;
   const uint64_t first_nz = __ballot(tb != 0);
@@ -2802,7 +2827,7 @@ __device__ __forceinline__ void resolve_item(const ResolveArgs &r, uint64_t item
   }
   if ((claimers >> lane) & 1) {
     const bool two = f2 && first_nz && (lane == __builtin_ctzll(first_nz));
-    score_row(r.hnb32, row, two ? 2u : 1u);
+    if (have < (two ? 2u : 1u)) score_row(r.hnb32, row, two ? 2u : 1u);
   }
 }
 
@@ -3347,11 +3372,17 @@ __global__ __launch_bounds__(256) void k_fin(FinArgs a) {
   const uint32_t wave = gtid >> 6;
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   const uint32_t cnt = min(a.counters[0], a.cap);  // k_tail's appends: an earlier launch
+  // stamp build: k_fin's waves are records kFinStampBase + wave (phases: windows, byte-item
+  // flushes, the rest of the item loop, the ticket / copy)
+  KBZ_TAIL_DECL;
+  const uint32_t fin_id = kFinStampBase + wave;
+  (void)fin_id;
   if (cnt == 0) {
     fin_copy_rows(a, 4 * gtid, 4 * gridDim.x * blockDim.x);
     if (blockIdx.x == 0) fin_rearm(a);
     return;
   }
+  KBZ_TAIL_MARK();
   // kClaimQ items per wave per round: byte items go through the claim queue (their rows' bytes
   // in flight together, as k_scan's inline claims), window items one at a time
   const int lane = threadIdx.x & 63;
@@ -3376,15 +3407,21 @@ __global__ __launch_bounds__(256) void k_fin(FinArgs a) {
         continue;
       }
       if ((item & 0xff) == 0) {
+        KBZ_TAIL_PH(2);
         resolve_item(a.ra, item);  // window item
+        KBZ_TAIL_ADD(win, 1);
+        KBZ_TAIL_PH(0);
       } else {
+        KBZ_TAIL_ADD(claims, 1);
         if (lane == 0)
           cq.q[cq.m] = make_uint4(item_chunk(item), (uint32_t)(item >> 11) & 0xffffff,
                                   (uint32_t)item & 0x1ff, (uint32_t)(item >> 9) & 3);
         cq.m++;
       }
     }
+    KBZ_TAIL_PH(2);
     claims_flush(ca, cq);
+    KBZ_TAIL_PH(1);
   }
   // The last kFinCopiers workgroups to arrive copy the rows together once every workgroup has
   // arrived: they only wait for workgroups that already hold a ticket or are still to be
@@ -3401,6 +3438,8 @@ __global__ __launch_bounds__(256) void k_fin(FinArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  KBZ_TAIL_PH(3);
+  KBZ_TAIL_END(fin_id);
   if (last < 0) return;
   fin_copy_rows_sc1(a, (uint32_t)last, nc);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3489,8 +3528,8 @@ __global__ __launch_bounds__(KBZ_SMALL_TPB) void k_small(SmallArgs a) {
       const uint64_t v0 = (uint64_t)vk.x | ((uint64_t)vk.y << 32), v1 = (uint64_t)vk.z | ((uint64_t)vk.w << 32);
       const bool any = ((t0 & v0) | (t1 & v1)) != 0;
       // has_new_bits' 2: a nonzero byte of the trace where the virgin byte is still 0xff
-      const bool two = ((nonzero_bytes8(t0) & ~nonzero_bytes8(~v0)) |
-                        (nonzero_bytes8(t1) & ~nonzero_bytes8(~v1))) != 0;
+      const bool two = ((nonzero_hi8(t0) & ~nonzero_hi8(~v0)) |
+                        (nonzero_hi8(t1) & ~nonzero_hi8(~v1))) != 0;
       vk = make_uint4(vk.x & ~t.x, vk.y & ~t.y, vk.z & ~t.z, vk.w & ~t.w);
       if (k == 0) v[0] = vk;
       else if (k == 1) v[1] = vk;

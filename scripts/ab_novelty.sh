@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out/abn
 for v in ${VARIANTS:-base}; do
-  lib=build_variants/$v/libkbz_hip.so
+  lib=build_variants/${v%_2}/libkbz_hip.so
   case $v in base*) lib=killerbeez_amd/libkbz_hip.so;; esac
   KBZ_HIP_LIB=$PWD/$lib timeout -k 10 300 python bench.py --no-cpu --no-pmc --no-ktrace --steps ${STEPS:-20} \
     --warmup 5 ${BENCH_ARGS:-} > gpurun_out/abn/$v.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/abn/$v.log; exit 1; }
