@@ -559,11 +559,13 @@ def novelty_heavy(args, mode, want, batches, dev, steps=8):
                     "stage_ms from one extra untimed step with stage events"}
 
 
-def sharded_world1(args, ctx, batches, counts, want, dev, timed, fused_ms):
-    """The N > 1 step at N = 1: the same fresh batches through dist.triage_sharded with
+def sharded_world1(args, ctx, batches, counts, want, dev, snap, fused_ms):
+    """The N > 1 step at N = 1: the headline's fresh batches through dist.triage_sharded with
     force_collective on a one-rank RCCL communicator (both all-gathers run), so the protocol's
     cost over the fused one-shard step is measured on a one-GPU box; phase times from HIP
-    events around each phase."""
+    events around each phase.  Each timed pass starts from `snap` (the virgin maps and last hash
+    the headline's timed steps started from), so it does the headline's work: the same batches,
+    never seen, in the same order."""
     import torch
     import torch.distributed as dist
 
@@ -580,12 +582,18 @@ def sharded_world1(args, ctx, batches, counts, want, dev, timed, fused_ms):
             triage_sharded(ctx, t, oc, counts[:1], 0, 1, want, device=dev, timings=log,
                            force_collective=True)
 
+        def restore():
+            torch.cuda.synchronize()
+            ctx.set_virgin(snap[0])
+            ctx.last_hash = snap[1]
+            torch.cuda.synchronize()
+
         # warm the communicator and the staged kernels, then the timed steps (phase events on)
         for t, oc in batches[:2]:
             sharded_step(t, oc)
         torch.cuda.synchronize()
         log.clear()
-        torch.cuda.synchronize()
+        restore()
         t0 = time.perf_counter()
         for i in range(args.steps):
             sharded_step(*batches[i % len(batches)])
@@ -593,7 +601,7 @@ def sharded_world1(args, ctx, batches, counts, want, dev, timed, fused_ms):
         el_box["s"] = time.perf_counter() - t0
         phases = timing_summary(log)
         # the same steps without phase events (the events add their own gaps)
-        torch.cuda.synchronize()
+        restore()
         t0 = time.perf_counter()
         for i in range(args.steps):
             triage_sharded(ctx, *batches[i % len(batches)], counts[:1], 0, 1, want, device=dev,
@@ -605,9 +613,10 @@ def sharded_world1(args, ctx, batches, counts, want, dev, timed, fused_ms):
                 "ms_per_step_with_phase_events": round(1e3 * el_box["s"] / args.steps, 4),
                 "phase_ms": {k: round(v, 4) for k, v in phases.items()},
                 "backend": dist.get_backend(),
-                "what": "the fresh batches again through triage_sharded(force_collective=True) on "
-                        "a one-rank RCCL group (the N>1 step's kernels and both all-gathers), "
-                        "virgin carried; fused_ms_per_step = the headline's step"}
+                "what": "the headline's fresh batches through triage_sharded(force_collective="
+                        "True) on a one-rank RCCL group (the N>1 step's kernels and both "
+                        "all-gathers), each pass from the virgin maps and last hash the headline "
+                        "started from; fused_ms_per_step = the headline's step"}
     except Exception as e:  # noqa: BLE001
         return {"error": f"{type(e).__name__}: {e}"[:300]}
 
@@ -679,6 +688,11 @@ def main_triage(args, pre):
     stage_ms = {k2: round(v / max(1, nb), 4) for k2, v in st.items()}
     fresh = pool[args.warmup:] if npool > args.warmup else pool
     phase_log = [] if world > 1 else None
+    # the state the timed fresh steps start from (the sharded variant replays them from it)
+    snap = None
+    if world == 1 and not args.no_variants and not dense:
+        torch.cuda.synchronize()
+        snap = (ctx.get_virgin(), ctx.last_hash)
     elapsed, pass1_ms = timed(fresh, args.steps)
     pass1_timed = timed_launches[-1]
     phases = timing_summary(phase_log) if phase_log else {}
@@ -692,6 +706,9 @@ def main_triage(args, pre):
                 "last_fresh_batch_work": fresh_stats,
                 "stage_ms_per_step": stage_ms,
                 "stage_ms_note": "fresh warmup batches 2..W, stage events on (off in the timed steps)"}
+    if snap is not None:  # before the variants below mutate or re-triage the batches
+        variants["sharded_protocol_world1"] = sharded_world1(
+            args, ctx, fresh[:args.steps], counts, want, dev, snap, ms_per_step)
     if not args.no_variants:
         seen = pool[-2:]
         el2, p2 = timed(seen, args.steps)
@@ -717,9 +734,6 @@ def main_triage(args, pre):
         if world == 1:
             variants["afl_all_crash_simplify"] = crash_variant(args, pool, barrier_sync, dev)
             variants["novelty_heavy"] = novelty_heavy(args, mode, want, fresh, dev)
-            if not dense:
-                variants["sharded_protocol_world1"] = sharded_world1(
-                    args, ctx, fresh, counts, want, dev, timed, 1e3 * elapsed / args.steps)
     del pool, fresh
     traffic = pre["traffic"]
     if traffic is None:
