@@ -2689,8 +2689,15 @@ __global__ __launch_bounds__(256) void k_scan(uint8_t *chunk_or, const uint8_t *
 // `acc`: row r claims t_r & V & ~(prev | acc) (has_new_bits, afl_instrumentation.c:600-662, over
 // the window), and scores 2 if it is the first row with a nonzero byte where V is 0xff and prev
 // is 0 (:644-651).  Rows are loaded KBZ_WIN_ROWS at a time (1 KiB per row, coalesced).
-#ifndef KBZ_WIN_ROWS  // rows of a window item in flight per round trip (8: novelty-heavy k_fin
-#define KBZ_WIN_ROWS 16  // spent 8 round trips per item)
+#ifndef KBZ_WIN_PIPE  // window items: the next WR rows' loads issued before the current WR rows
+#define KBZ_WIN_PIPE 1  // are processed (two register groups); 0: load, wait, process
+#endif
+#ifndef KBZ_WIN_ROWS  // rows of a window item per group (unpipelined: in flight per round trip;
+#if KBZ_WIN_PIPE     // 8 spent 8 round trips per item on novelty-heavy k_fin).  Pipelined, two
+#define KBZ_WIN_ROWS 8  // groups of 8 are in flight (k_fin 186 VGPRs: 2 waves per SIMD; two
+#else                   // groups of 16 take 308)
+#define KBZ_WIN_ROWS 16
+#endif
 #endif
 struct ResolveArgs {  // what resolving a claim item needs (k_resolve, the fused tail)
   const uint8_t *traces;
@@ -2749,19 +2756,21 @@ __device__ __forceinline__ void resolve_window_xf(const ResolveArgs &r, uint32_t
   constexpr uint64_t kHi = 0x8080808080808080ull;
   const uint64_t ff0 = ~nonzero_hi8(~vr0) & kHi, ff1 = ~nonzero_hi8(~vr1) & kHi;
   bool claimed = false;
-  while (rows) {
-    constexpr int WR = KBZ_WIN_ROWS;
-    int rr[WR];
-    uint4 v[WR];
-    // lane l: row l's score so far (refreshed every round trip, with the rows' loads)
-    const uint32_t have = (KBZ_SCORE_SKIP && rl < r.n) ? ld_sc1(&r.hnb32[rl]) : 0u;
+  constexpr int WR = KBZ_WIN_ROWS;
+  // the next WR rows' loads (and, lane l, row l's score so far: a row whose score already covers
+  // this window's needs no atomic)
+  auto issue = [&](int (&rr)[WR], uint4 (&v)[WR], uint32_t &have) {
+    have = (KBZ_SCORE_SKIP && rl < r.n) ? ld_sc1(&r.hnb32[rl]) : 0u;
 #pragma unroll
-    for (int u = 0; u < WR; u++) {  // up to WR rows' loads in flight
+    for (int u = 0; u < WR; u++) {
       rr[u] = rows ? __builtin_ctzll(rows) : -1;
       rows &= rows - 1;
       const uint64_t rw = row0 + (rr[u] >= 0 ? rr[u] : 0);
       v[u] = act ? *(const uint4 *)(r.traces + rw * r.stride + cl) : make_uint4(0, 0, 0, 0);
     }
+  };
+  // those rows in order: new bits against the running OR, the "2" test, the score
+  auto process = [&](const int (&rr)[WR], const uint4 (&v)[WR], uint32_t have) {
 #pragma unroll
     for (int u = 0; u < WR; u++) {
       if (rr[u] < 0) break;  // wave-uniform
@@ -2779,7 +2788,38 @@ __device__ __forceinline__ void resolve_window_xf(const ResolveArgs &r, uint32_t
           score_row(r.hnb32, row0 + rr[u], sc);
       }
     }
+  };
+#if KBZ_WIN_PIPE
+  // two register groups: a group's loads are in flight while the previous group is processed
+  if (rows) {
+    int rA[WR], rB[WR];
+    uint4 vA[WR], vB[WR];
+    uint32_t hA, hB;
+    issue(rA, vA, hA);
+    while (true) {  // wave-uniform
+      if (!rows) {
+        process(rA, vA, hA);
+        break;
+      }
+      issue(rB, vB, hB);
+      process(rA, vA, hA);
+      if (!rows) {
+        process(rB, vB, hB);
+        break;
+      }
+      issue(rA, vA, hA);
+      process(rB, vB, hB);
+    }
   }
+#else
+  while (rows) {
+    int rr[WR];
+    uint4 v[WR];
+    uint32_t have;
+    issue(rr, v, have);
+    process(rr, v, have);
+  }
+#endif
   if (!claimed && lane == 0) atomicOr(r.err, 8u);  // k_scan saw new bits here: inconsistent
 }
 __device__ __forceinline__ void resolve_window(const ResolveArgs &r, uint32_t chunk, int k,
