@@ -175,12 +175,16 @@ int kbz_triage_batch_host(kbz_ctx_t *ctx, const uint8_t *traces, size_t n, size_
  *     batch's whole copy waits for the submit.  A slot with committed rows is always triaged
  *     from device memory (batches of <= 64 uncommitted rows are read from the pinned slot).
  *   kbz_ring_flush: waits for every submitted batch, delivers results, reports device errors.
+ *   kbz_ring_release: hands the acquired slot back untriaged (its rows were consumed elsewhere,
+ *     e.g. by kbz_triage_batch_devices, which reads pinned rows by DMA); the next acquire may
+ *     return the same slot.
  * Do not interleave with kbz_triage_batch_host on the same context (they share the slots). */
 int kbz_ring_acquire(kbz_ctx_t *ctx, uint8_t **rows, int8_t **outcome, size_t *cap);
 int kbz_ring_commit(kbz_ctx_t *ctx, size_t n_ready);
 int kbz_ring_submit(kbz_ctx_t *ctx, size_t n, int have_outcome, uint8_t *hnb_out,
                     uint32_t *h32_out, uint64_t *x64_out, int want);
 int kbz_ring_flush(kbz_ctx_t *ctx);
+int kbz_ring_release(kbz_ctx_t *ctx);
 
 /* ---- sharded (multi-GPU) triage ------------------------------------------------------------ */
 /* A batch split into contiguous shards, one per GPU (rank g holds traces [lo_g, hi_g)), gives
@@ -304,7 +308,9 @@ int kbz_merge_and_fill_devices(uint8_t *out, size_t n, size_t state_bytes, kbz_m
  * has_new_bits / has_new_coverage -- and every worker's virgin maps and last hash become that
  * pass's.  XXH64 is not offered here (KBZ_WANT_X64 fails).  Synchronous.
  * Host batches are staged per worker on the worker's own host thread through two pinned slots
- * (the host copy of one slot overlaps the DMA of the other), all workers at once.
+ * (the host copy of one slot overlaps the DMA of the other), all workers at once; a batch that
+ * already lies in pinned host memory (hipHostMalloc / hipHostRegister, e.g. a ring slot) goes to
+ * each worker by DMA straight from there.
  * kbz_mctx_create enables peer access between every pair of the workers' distinct devices
  * (hipDeviceEnablePeerAccess) so the exchanges' peer copies run over xGMI;
  * kbz_mctx_peer_pairs returns how many ordered device pairs have it (0 on one GPU).

@@ -39,6 +39,7 @@ SIGNATURES = [
     ("kbz_ring_acquire", _i, [_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_sz)]),
     ("kbz_ring_submit", _i, [_vp, _sz, _i, _vp, _vp, _vp, _i]),
     ("kbz_ring_flush", _i, [_vp]),
+    ("kbz_ring_release", _i, [_vp]),
     ("kbz_ring_commit", _i, [_vp, _sz]),
     ("kbz_shard_begin", _i, [_vp, _vp, _sz, _sz, _vp, _vp, _vp, _i, _vp]),
     ("kbz_shard_last_hash", _i, [_vp, _vp, _vp]),

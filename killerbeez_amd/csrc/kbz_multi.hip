@@ -451,13 +451,25 @@ void fill_rows(uint8_t *dst, const uint8_t *src, size_t rows, size_t stride, siz
   for (auto &t : th) t.join();
 }
 
+// Host memory the runtime pinned (hipHostMalloc / hipHostRegister): its DMA needs no staging.
+bool pinned_host(const void *p) {
+  hipPointerAttribute_t at;
+  const bool ok = hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost;
+  (void)hipGetLastError();  // pageable memory: an "invalid value" that is no error here
+  return ok;
+}
+
 // Worker w's host shard (nw rows) to its device rows m->traces[w] through its two pinned slots:
-// the host copy of slot i overlaps the DMA of slot i ^ 1.  Runs on the worker's own thread.
+// the host copy of slot i overlaps the DMA of slot i ^ 1.  Runs on the worker's own thread.  A
+// shard already in pinned memory (e.g. the plugin's ring slot) is copied by the DMA engine
+// straight from there.
 int stage_shard(kbz_mctx *m, size_t w, const uint8_t *src, size_t nw, size_t stride,
-                const int8_t *oc, int threads) {
+                const int8_t *oc, int threads, bool pinned) {
   const size_t M = m->M, R = m->stage_rows;
   MHIP(hipSetDevice(m->dev[w]));
-  for (size_t r0 = 0, i = 0; r0 < nw; r0 += R, i++) {
+  if (pinned && nw)
+    MHIP(hipMemcpy2DAsync(m->traces[w], M, src, stride, M, nw, hipMemcpyHostToDevice, m->s[w]));
+  for (size_t r0 = 0, i = 0; !pinned && r0 < nw; r0 += R, i++) {
     const int sl = (int)(i & 1);
     const size_t cnt = std::min(R, nw - r0);
     MHIP(hipEventSynchronize(m->ev_slot[sl][w]));  // the slot's previous DMA is done
@@ -571,9 +583,10 @@ extern "C" int kbz_triage_batch_devices(kbz_mctx_t *m, const uint8_t *traces, si
   const int per = std::max(1, 8 / (int)W);
   std::vector<int> rc(W, 0);
   std::vector<std::string> err(W);
+  const bool pinned = n && pinned_host(traces);
   auto job = [&](size_t w) {
     if (stage_shard(m, w, traces + lo[w] * stride, cnt[w], stride, outcome ? outcome + lo[w] : nullptr,
-                    per)) {
+                    per, pinned)) {
       rc[w] = -1;
       err[w] = kbz_last_error();
     }

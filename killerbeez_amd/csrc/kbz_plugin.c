@@ -138,6 +138,13 @@ typedef struct kbz_plugin {
   unsigned long dump_failures;  /* dump_map_dir / get_module_info bookkeeping that failed */
   int early_copy;          /* start large windows' host-to-device copy while recording (default
                             * 1; KBZ_PLUGIN_EARLY_COPY=0 for A/B runs) */
+  /* option "devices" ("0,1,2,3"): windows and batches of at least shard_min execs (option
+   * "shard_min", default 1024) are triaged sharded over these GPUs (kbz_triage_batch_devices,
+   * one host thread per GPU); the plugin's own context keeps the smaller ones.  The state moves
+   * through the host mirror around every sharded batch, so both always agree. */
+  int *shard_dev;
+  size_t shard_ndev, shard_min;
+  kbz_mctx_t *shard;
 } kbz_plugin_t;
 
 static size_t nmaps(const kbz_plugin_t *p) { return p->mode == KBZ_MODE_DYNAMORIO ? 1 : 3; }
@@ -406,6 +413,8 @@ static char *put_hex(char *o, const uint8_t *b, size_t n) {
 /* ---- lifetime ------------------------------------------------------------------------------ */
 static void plugin_free(kbz_plugin_t *p) {
   if (!p) return;
+  if (p->shard) kbz_mctx_destroy(p->shard);
+  free(p->shard_dev);
   if (p->ctx) kbz_ctx_destroy(p->ctx);
   for (size_t m = 0; m < p->nmod; m++) {
     if (p->mctx && p->mctx[m]) kbz_ctx_destroy(p->mctx[m]);
@@ -525,6 +534,51 @@ static kbz_plugin_t *plugin_dump_alloc(kbz_plugin_t *p) {
   return p;
 }
 
+/* "devices": comma-separated GPU ordinals (repeats allowed: workers sharing a GPU),
+ * "shard_min": the smallest batch that is sharded (>= 1).  Sharded windows are never split into
+ * afl_gpu's early sub-batches, and their rows are not copied early: the whole window goes to the
+ * workers at once. */
+static int plugin_shard_options(kbz_plugin_t *p, const char *options) {
+  unsigned long long smin = 1024;
+  if (json_u64(options, "shard_min", &smin) < 0 || smin < 1) {
+    set_err("bad options (shard_min must be an integer >= 1)");
+    return -1;
+  }
+  p->shard_min = (size_t)smin;
+  const int given = options && json_value(options, "devices");
+  char *devs = given ? json_str(options, "devices") : NULL;
+  if (given && !devs) {
+    set_err("devices must be a string of comma-separated GPU ordinals");
+    return -1;
+  }
+  if (!devs) return 0;
+  size_t n = 1;
+  for (const char *c = devs; *c; c++) n += *c == ',';
+  p->shard_dev = (int *)calloc(n, sizeof(int));
+  if (!p->shard_dev) {
+    free(devs);
+    set_err("out of host memory");
+    return -1;
+  }
+  const char *c = devs;
+  for (size_t i = 0; i < n; i++) {
+    char *end = NULL;
+    const long d = strtol(c, &end, 10);
+    if (end == c || d < 0 || (*end && *end != ',')) {
+      free(devs);
+      set_err("devices must be a string of comma-separated GPU ordinals");
+      return -1;
+    }
+    p->shard_dev[i] = (int)d;
+    c = *end ? end + 1 : end;
+  }
+  free(devs);
+  p->shard_ndev = n;
+  p->sub_k = 0;
+  p->early_copy = 0;
+  return 0;
+}
+
 static kbz_plugin_t *plugin_from_options(int mode, const char *options) {
   unsigned long long m = 65536, mb = 4096;
   if (options && !json_valid_object(options)) {
@@ -613,6 +667,10 @@ static kbz_plugin_t *plugin_from_options(int mode, const char *options) {
       plugin_free(p);
       return NULL;
     }
+  }
+  if (plugin_shard_options(p, options)) {
+    plugin_free(p);
+    return NULL;
   }
   return plugin_dump_alloc(p);
 }
@@ -743,6 +801,48 @@ static int sync_mirror(kbz_plugin_t *p) {
   return 0;
 }
 
+/* A batch of the plugin's own execs sharded over the "devices" GPUs: the state goes to every
+ * worker from the host mirror (the plugin's context is synced into it first), the sharded
+ * protocol runs (kbz_triage_batch_devices: synchronous), and the resulting state comes back into
+ * the mirror and the plugin's context.  Rows in pinned memory (the ring slot) go to the workers
+ * by DMA straight from there. */
+static int shard_batch(kbz_plugin_t *p, const uint8_t *rows, size_t n, size_t stride,
+                       const int8_t *outcome, uint8_t *hnb, uint32_t *h32) {
+  if (!p->shard) {
+    p->shard = kbz_mctx_create(p->map_size, p->mode, p->max_batch, p->shard_dev, p->shard_ndev);
+    if (!p->shard) {
+      set_err("GPU shards: %s", kbz_last_error());
+      return -1;
+    }
+    for (size_t w = 0; p->ignore && w < p->shard_ndev; w++)
+      if (kbz_set_ignore(kbz_mctx_worker(p->shard, w), p->ignore)) {
+        set_err("GPU shards (ignore bytes): %s", kbz_last_error());
+        return -1;
+      }
+  }
+  if (sync_mirror(p)) return -1;
+  for (size_t w = 0; w < p->shard_ndev; w++) {
+    kbz_ctx_t *c = kbz_mctx_worker(p->shard, w);
+    if (kbz_set_virgin(c, p->virgin) || kbz_set_last_hash(c, p->last_hash)) {
+      set_err("GPU shards (state upload): %s", kbz_last_error());
+      return -1;
+    }
+  }
+  const int want = h32 ? KBZ_WANT_H32 : 0;
+  if (kbz_triage_batch_devices(p->shard, rows, n, stride, outcome, hnb, h32, want) ||
+      kbz_mctx_get_virgin(p->shard, p->virgin) || kbz_mctx_get_last_hash(p->shard, &p->last_hash) ||
+      kbz_set_virgin(p->ctx, p->virgin) || kbz_set_last_hash(p->ctx, p->last_hash)) {
+    set_err("GPU shards: %s", kbz_last_error());
+    p->mirror_stale = 1;
+    return -1;
+  }
+  p->mirror_stale = 0;
+  return 0;
+}
+static int shard_eligible(const kbz_plugin_t *p, size_t n, int want_x64) {
+  return p->shard_ndev && !p->per_module && !want_x64 && n >= p->shard_min;
+}
+
 /* classify_counts (dynamorio_instrumentation.c:246-292: count_class_lookup8 over each byte) for
  * the side outputs that need one classified map at a time -- a dump_map_dir file, get_module_info's
  * info -- on the host: the novelty path itself never runs here. */
@@ -863,6 +963,19 @@ static int plugin_flush(kbz_plugin_t *p) {
       return -1;
     }
     for (size_t i = 0; i < p->nmod; i++) p->mnew[i] = p->r_mhnb[i * n + n - 1] != 0;
+  } else if (!off && shard_eligible(p, nq, 0)) {
+    /* the window sharded over the "devices" GPUs, read from the pinned slot; the slot is handed
+     * back to the ring empty */
+    if (shard_batch(p, rows, nq, p->map_size, p->q_outcome, p->w_hnb,
+                    p->dump_dir ? p->r_h32 : NULL))
+      return -1;
+    if (kbz_ring_release(p->ctx) || kbz_ring_flush(p->ctx)) {
+      set_err("GPU ring: %s", kbz_last_error());
+      return -1;
+    }
+    uint8_t *t = p->r_hnb;
+    p->r_hnb = p->w_hnb;
+    p->w_hnb = t;
   } else {
     /* the slot's rows (after any sub-batches: AFL, no hashes), results into the window's buffer;
      * the flush delivers every part, then the window's buffer becomes the queryable one */
@@ -997,11 +1110,18 @@ static int plugin_triage_batch(kbz_plugin_t *p, const uint8_t *traces, size_t n,
   for (size_t lo = 0; lo < n; lo += p->max_batch) {
     const size_t cnt = n - lo < p->max_batch ? n - lo : p->max_batch;
     uint32_t *hb = h32 ? h32 + lo : p->dump_dir ? p->r_h32 : NULL;
-    if (kbz_triage_batch_host(p->ctx, traces + lo * stride, cnt, stride,
-                              outcome ? outcome + lo : NULL, hnb ? hnb + lo : NULL, hb,
-                              x64 ? x64 + lo : NULL, want)) {
-      set_err("GPU triage: %s", kbz_last_error());
-      return -1;
+    if (shard_eligible(p, cnt, x64 != NULL)) {
+      if (shard_batch(p, traces + lo * stride, cnt, stride, outcome ? outcome + lo : NULL,
+                      hnb ? hnb + lo : p->r_hnb, hb))
+        return -1;
+    } else {
+      p->mirror_stale = 1;  /* (a sharded chunk before this one left the mirror current) */
+      if (kbz_triage_batch_host(p->ctx, traces + lo * stride, cnt, stride,
+                                outcome ? outcome + lo : NULL, hnb ? hnb + lo : NULL, hb,
+                                x64 ? x64 + lo : NULL, want)) {
+        set_err("GPU triage: %s", kbz_last_error());
+        return -1;
+      }
     }
     if (p->dump_dir && hb != p->r_h32) memcpy(p->r_h32, hb, cnt * sizeof(uint32_t));
     plugin_window_done(p, traces + lo * stride, cnt, stride);

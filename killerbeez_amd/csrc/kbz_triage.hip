@@ -5363,6 +5363,13 @@ int kbz_ring_commit(kbz_ctx_t *c, size_t n_ready) {
   return 0;
 }
 
+int kbz_ring_release(kbz_ctx_t *c) {
+  if (!c) return fail("null ctx");
+  if (c->ring_acquired < 0) return fail("kbz_ring_release: no slot acquired");
+  c->ring_acquired = -1;  // untouched by the GPU: the next acquire may hand it out again
+  return 0;
+}
+
 int kbz_ring_flush(kbz_ctx_t *c) {
   if (!c) return fail("null ctx");
   if (!c->work_stream) return 0;  // nothing was ever submitted

@@ -9,6 +9,7 @@ at a time, is_new_path after each) and in deferred/batched form, bit-exact again
 sequential per-exec loop; state dump/load and the merger fold against the oracle.
 """
 import ctypes as C
+import json
 import os
 
 import numpy as np
@@ -249,6 +250,47 @@ def test_afl_sub_batched_windows(gpu, monkeypatch, sub_k):
     np.testing.assert_array_equal(maps["virgin_bits"], exp["virgin"][0])
     np.testing.assert_array_equal(maps["virgin_tmout"], exp["virgin"][1])
     np.testing.assert_array_equal(maps["virgin_crash"], exp["virgin"][2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,mode", MODES)
+def test_sharded_windows_and_batches(gpu, name, mode):
+    """Option "devices" (here two workers on one GPU, "0,0") with shard_min 64: recorded windows
+    of 100 and 256 execs and a triage_batch of 300 (chunks of max_batch 256 and 44) go through
+    kbz_triage_batch_devices, a window of 30 and the batch's last 44 through the plugin's own
+    context; repeats at the window and shard boundaries (the DynamoRIO last-hash skip across
+    them).  Results and the final state equal the per-exec ones."""
+    wins = [100, 30, 256]
+    n = sum(wins) + 300
+    t, oc = synth.sparse_np(n, M, seed=41, hot_frac=0.05, outcome_p=(0.8, 0.1, 0.1))
+    for j in (100, 130, 130 + 128, 386, 386 + 150):  # window / shard starts repeat their predecessor
+        t[j] = t[j - 1]
+        oc[j] = oc[j - 1]
+    exp = _expected(mode, t, oc)
+    opts = json.dumps({"map_size": M, "max_batch": 256, "devices": "0,0", "shard_min": 64})
+    p = P.Plugin(name, opts)
+    got, lo = [], 0
+    for w in wins:
+        tickets = [p.record(t[j], int(oc[j])) for j in range(lo, lo + w)]
+        got += [p.result(k) for k in tickets]
+        assert p.is_new_path() == int(exp["hnb"][lo + w - 1] != 0)
+        lo += w
+    r = p.triage_batch(t[lo:], oc[lo:], hashes=False)
+    np.testing.assert_array_equal(np.array(got, np.uint8), exp["hnb"][:lo])
+    np.testing.assert_array_equal(r["hnb"], exp["hnb"][lo:])
+    maps = P.state_maps(p.get_state(), M)
+    np.testing.assert_array_equal(maps["virgin_bits"], exp["virgin"][0])
+    if name == "afl_gpu":
+        np.testing.assert_array_equal(maps["virgin_tmout"], exp["virgin"][1])
+        np.testing.assert_array_equal(maps["virgin_crash"], exp["virgin"][2])
+    else:
+        assert maps["last_shm_hash"] == exp["last_hash"]
+
+
+def test_shard_options_are_checked():
+    for bad in ('{"devices": 3}', '{"devices": "0,x"}', '{"devices": "-1"}', '{"shard_min": 0}'):
+        with pytest.raises(RuntimeError):
+            P.Plugin("afl_gpu", bad)
 
 
 @pytest.mark.gpu
