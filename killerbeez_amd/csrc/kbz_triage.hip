@@ -4511,8 +4511,12 @@ int shard_begin_impl(kbz_ctx *c, const uint8_t *traces, size_t n, size_t stride,
   a.rflags = nullptr;
   a.epoch = 0;
   c->cur_rec = false;
-  // one-shard DynamoRIO batches through k_pass1s without ignore bytes or XXH64: claim records
-  if (fused && c->rec_ok && p1s_records(c->mode, c->ignore != nullptr, a.x64 != nullptr) &&
+  // DynamoRIO batches through k_pass1s without ignore bytes or XXH64 (one-shard batches and
+  // shards): claim records.  A shard's row 0 is linked later (k_chain), but a record never needs
+  // it: a row 0 that repeats its predecessor holds only bits of the prefix (the earlier shards'
+  // aggregate holds the predecessor's), so it is never a claim's first holder, and a row 0 that
+  // differs (a collision) puts its chunk on the fix list, whose claims read the rows.
+  if (c->rec_ok && p1s_records(c->mode, c->ignore != nullptr, a.x64 != nullptr) &&
       !pass1_is_wide(c->pass1, c->cur_chunks)) {
     if (!c->frec) {
       const size_t bytes = (size_t)c->max_chunks * c->M * sizeof(uint64_t);
@@ -5003,7 +5007,9 @@ int kbz_shard_finish_gathered(kbz_ctx_t *c, const uint8_t *d_gathered, size_t ra
   a.win_items = c->win_items;
   a.inline_max = c->inline_max;
   a.tail = c->tail;
-  a.frec = nullptr;  // shards record no claims in pass 1
+  a.frec = c->cur_rec ? c->frec : nullptr;  // pass 1's claim records (see shard_begin_impl)
+  a.rflags = c->rflags;
+  a.epoch = c->epoch;
   a.shard_last = c->shard_last;
   a.neq = c->neq;
   a.bad_list = c->bad_list;
