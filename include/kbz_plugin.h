@@ -30,7 +30,10 @@
  * Options (create's JSON string; every key optional):
  *   {"map_size": 65536, "max_batch": 4096}; dynamorio_gpu also "ignore_bytes_file": "<path>",
  *   "per_module_coverage": 0/1, "coverage_modules": [names], "ignore_bytes_dir": "<dir>",
- *   "dump_map_dir": "<dir>" (dynamorio_instrumentation.c:1040-1051)
+ *   "dump_map_dir": "<dir>" (dynamorio_instrumentation.c:1040-1051); both plugins "devices":
+ *   "0,1,..." (GPU ordinals, repeats allowed) and "shard_min": 1024 -- windows / triage_batch
+ *   chunks of at least shard_min execs are sharded over those GPUs (kbz_triage_batch_devices),
+ *   smaller ones stay on the plugin's own GPU context (not with per_module_coverage)
  * State (get_state / set_state / create's state argument), keys as the reference's
  * afl_get_state :62-79 and dynamorio_get_state :1239-1281:
  *   afl_gpu       {"map_size": M, "virgin_bits": "<hex>", "virgin_tmout": "<hex>",
